@@ -1,0 +1,50 @@
+# Build: product library (gfx950 HIP + host C++), oracle (plain C, test
+# infrastructure), C++ parity test.  No cmake: hipcc / gcc directly.
+HIPCC   ?= /opt/rocm/bin/hipcc
+CC      ?= gcc
+CXX     ?= g++
+ARCH    ?= gfx950
+BUILD   := build
+
+INC      := -Iinclude -Icyclone_amd/csrc
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result $(INC)
+HOSTFLAGS:= -O2 -std=c++17 -fPIC -Wall $(INC) -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
+
+LIB      := cyclone_amd/libcyaes.so
+ORACLE   := oracle/liboracle.so
+CPPTEST  := $(BUILD)/test_rijndael
+
+KSRC     := cyclone_amd/csrc/cyaes_kernels.hip
+HSRC     := cyclone_amd/csrc/cyaes_runtime.cpp cyclone_amd/csrc/cyaes_tables.cpp cyclone_amd/csrc/cyr_rijndael.cpp
+HDRS     := include/cyaes.h include/cyclone_amd/cyr_rijndael.h cyclone_amd/csrc/cyaes_internal.h \
+            cyclone_amd/csrc/cyaes_tables.h
+
+KOBJ     := $(BUILD)/cyaes_kernels.o
+HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
+
+.PHONY: all lib oracle cpptest clean
+all: lib oracle cpptest
+lib: $(LIB)
+oracle: $(ORACLE)
+cpptest: $(CPPTEST)
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+$(KOBJ): $(KSRC) $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/%.o: cyclone_amd/csrc/%.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
+
+$(LIB): $(KOBJ) $(HOBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
+
+$(ORACLE): oracle/aes_oracle.c
+	$(CC) -O2 -fPIC -shared -pthread -Wall -o $@ $<
+
+$(CPPTEST): tests/cpp/test_rijndael.cpp $(LIB) $(HDRS)
+	$(CXX) -O2 -std=c++17 -Wall $(INC) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(ORACLE)

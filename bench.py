@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident AES-128-CBC encrypt+decrypt throughput on MI355X.
+
+Metric (BASELINE.json): "AES encrypt+decrypt GiB/s device-resident (64 KiB
+payloads); % HBM roofline @1/2/4/8 GPU".  One step = one CBC-encrypt pass
+plus one CBC-decrypt pass over the per-GPU batch (config C of BASELINE.json:
+1 key, 262,144 payloads x 65,536 B = 16 GiB per GPU; every payload an
+independent chain from DefaultIV, the relay semantics of
+relay_local.cpp:206 / relay_server.cpp:329).  value = 2 x bytes x steps x
+ranks / max-over-ranks wall time, in GiB/s (2^30).
+
+Multi-GPU (torchrun, one process per GPU): rank 0 holds the session key and
+broadcasts it over RCCL (xGMI); every rank expands it on its device and
+processes its own payload shard (weak scaling: per-GPU batch fixed, payload
+indices [rank*P, (rank+1)*P) of the global stream).  No data-path collective.
+
+cpu_baseline: the oracle (a plain-C restatement of the reference's scalar
+Rijndael, oracle/aes_oracle.c) timed on this host's cores on a bounded
+sample of the same workload, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "AES encrypt+decrypt GiB/s device-resident (64 KiB payloads); % HBM roofline @1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+PLAINTEXT_SEED = 0x5EEDC1C1
+CONFIGS = {
+    # name: (payloads per GPU, payload bytes, payloads per session key (0 = one key))
+    "C": (262144, 65536, 0),
+    "B": (1048576, 1472, 0),
+    "D": (1048576, 1472, 256),
+    "A": (4096, 1024, 0),
+}
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C", choices=sorted(CONFIGS))
+    ap.add_argument("--payloads", type=int, default=0, help="override payloads per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="cpu baseline sample payloads (0 = auto)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def session_keys(n):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import struct
+    seed = 0xC1C10E55D0000000
+
+    def sm(x):
+        x = (x + 0x9E3779B97F4A7C15) & (2**64 - 1)
+        x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+        x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+        return x ^ (x >> 31)
+    return b"".join(struct.pack("<QQ", sm(seed + 2 * s), sm(seed + 2 * s + 1)) for s in range(n))
+
+
+def cpu_baseline(cfg_name, npay, pb, ppk, d_ct, torch):
+    """Oracle (scalar reference restatement) on the host cores; bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    sample = min(npay, int(max(1, (2 << 30) // pb)))  # ~2 GiB of payload
+    keys = [bytes(range(16))] if not ppk else [session_keys(sample // ppk + 1)[16 * s:16 * s + 16]
+                                              for s in range(sample // ppk + 1)]
+    pt = oracle.synthetic(0, sample, pb)
+    t0 = time.perf_counter()
+    ct = oracle.batch(False, keys, ppk, pt, pb, nthreads=threads)
+    t1 = time.perf_counter()
+    rt = oracle.batch(True, keys, ppk, ct, pb, nthreads=threads)
+    t2 = time.perf_counter()
+    # single-core figure on a smaller slice
+    s1 = max(1, sample // 32)
+    t3 = time.perf_counter()
+    ct1 = oracle.batch(False, keys, ppk, pt[:s1 * pb], pb, nthreads=1)
+    t4 = time.perf_counter()
+    oracle.batch(True, keys, ppk, ct1, pb, nthreads=1)
+    t5 = time.perf_counter()
+    torch.cuda.synchronize()
+    gpu_sample = d_ct[: sample * pb].cpu().numpy()
+    exact = bool(np.array_equal(gpu_sample, ct)) and bool(np.array_equal(rt, pt))
+    gib = float(1 << 30)
+    return {
+        "value": round(2 * sample * pb / (t2 - t0) / gib, 4),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": "config %s: first %d payloads x %d B (%.2f GiB), encrypt then decrypt, %d threads "
+                  "(one Rijndael key schedule per thread, as relay's work threads); oracle/aes_oracle.c"
+                  % (cfg_name, sample, pb, sample * pb / gib, threads),
+        "single_core": round(2 * s1 * pb / ((t4 - t3) + (t5 - t4)) / gib, 4),
+        "seconds": round(t2 - t0, 3),
+        "matches_gpu": exact,
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import cyclone_amd as ca
+
+    npay, pb, ppk = CONFIGS[args.config]
+    if args.payloads:
+        npay = args.payloads
+    nbytes = npay * pb
+    p0 = rank * npay
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    ctx = ca.GpuContext(local)
+    # Session key(s): rank 0 owns them (DH secret in the relay), RCCL-broadcast to all GPUs.
+    nkeys = (npay * world + ppk - 1) // ppk if ppk else 1
+    if rank == 0:
+        raw = session_keys(nkeys) if ppk else bytes(range(16))
+        d_keys = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda")
+    else:
+        d_keys = torch.zeros(16 * nkeys, dtype=torch.uint8, device="cuda")
+    if world > 1:
+        dist.broadcast(d_keys, src=0)
+    if ppk:  # this rank's sessions only
+        first = p0 // ppk
+        d_keys = d_keys[16 * first: 16 * (first + (npay + ppk - 1) // ppk)].contiguous()
+    ctx.set_keys_device(d_keys, d_keys.numel() // 16, sh)
+
+    log("rank %d/%d: config %s, %d payloads x %d B = %.2f GiB per GPU, %d CUs"
+        % (rank, world, args.config, npay, pb, nbytes / 2**30, ctx.num_cus))
+    d_pt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    d_ct = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    d_rt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    ctx.fill_synthetic(d_pt, p0, npay, pb, PLAINTEXT_SEED, sh)
+
+    def enc():
+        ctx.encrypt_uniform(d_pt, d_ct, npay, pb, payloads_per_key=ppk, stream=sh)
+
+    def dec():
+        ctx.decrypt_uniform(d_ct, d_rt, npay, pb, payloads_per_key=ppk, stream=sh)
+
+    for _ in range(args.warmup):
+        enc()
+        dec()
+    torch.cuda.synchronize()
+
+    parity = None
+    if not args.no_verify:
+        golden = json.load(open(os.path.join(ROOT, "tests", "golden", "openssl_vectors.json")))["configs"]
+        gname = {"C": "C", "B": "B", "D": "D", "A": "A"}[args.config] if rank == 0 else (
+            "E_rank1" if (rank == 1 and args.config == "C") else None)
+        dp = ctx.digest(d_pt, nbytes, sh)
+        dc = ctx.digest(d_ct, nbytes, sh)
+        dr = ctx.digest(d_rt, nbytes, sh)
+        ok = dr == dp
+        g = golden.get(gname) if gname else None
+        if g and g["npayloads"] == npay and g["payload_bytes"] == pb:
+            ok = ok and ["%016x" % v for v in dc] == g["cipher_digest"] and ["%016x" % v for v in dp] == g["plain_digest"]
+        ok = ok and ctx.check() == ca.CYAES_OK
+        flag = torch.tensor([0 if ok else 1], device="cuda")
+        if world > 1:
+            dist.all_reduce(flag)
+        parity = "bit-exact" if int(flag.item()) == 0 else "MISMATCH"
+        log("parity:", parity)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        enc()
+        ev[i][1].record(stream)
+        dec()
+        ev[i][2].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    t = float(elapsed.item())
+
+    enc_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps
+    dec_ms = sum(b.elapsed_time(c) for _, b, c in ev) / args.steps
+    gib = float(1 << 30)
+    value = 2.0 * nbytes * args.steps * world / t / gib
+
+    def roof(ms):
+        ach = 2.0 * nbytes / (ms / 1e3) / 1e9  # algorithmic: read N + write N per launch
+        return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4)}
+
+    kern = {"encrypt": dict(roof(enc_ms), avg_ms=round(enc_ms, 4)),
+            "decrypt": dict(roof(dec_ms), avg_ms=round(dec_ms, 4))}
+    dom = "encrypt" if enc_ms >= dec_ms else "decrypt"
+    roofline = dict(roof(enc_ms if dom == "encrypt" else dec_ms), kernel=dom, traffic=None)
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        tr = json.load(open(tfile)).get(args.config, {}).get(dom)
+        if tr:
+            roofline["traffic"] = tr.get("bytes_per_launch")
+            roofline["traffic_note"] = tr.get("note")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        log("cpu baseline ...")
+        cpu = cpu_baseline(args.config, npay, pb, ppk, d_ct, torch)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(t / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "config %s: %d payloads x %d B per GPU (%.2f GiB), %s, encrypt+decrypt, "
+                                   "device-resident, AES-128-CBC chain per payload from DefaultIV"
+                                   % (args.config, npay, pb, nbytes / gib,
+                                      ("%d payloads per session key" % ppk) if ppk else "1 key"),
+                       "payloads_per_gpu": npay, "payload_bytes": pb, "parallelism": "payload shards x%d, "
+                       "RCCL key broadcast" % world},
+            "hbm_frac_step": round(4.0 * nbytes * world / (t / args.steps) / 1e9 / (HBM_PEAK_GBS * world), 4),
+            "roofline": roofline, "kernels": kern, "cpu_baseline": cpu, "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

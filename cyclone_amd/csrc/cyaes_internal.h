@@ -1,0 +1,91 @@
+// cyaes_internal.h -- shared between the gfx950 kernels (cyaes_kernels.hip)
+// and the host runtime (cyaes_runtime.cpp).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cyaes {
+
+// Device key schedule: the reference's m_Ke / m_Kd words (cyr_rijndael.h:50,52)
+// byte-swapped to little-endian so a dwordx4 load of a block is directly the
+// cipher state.  88 words = 352 B per key, ek at [0,44), dk at [44,88).
+constexpr int kSchedWords = 88;
+
+// LDS image: 256 rows x 256 B.  Row x holds word A[x] in slots 0..31 and
+// word B[x] in slots 32..63 (one copy per bank), so lane l always reads bank
+// l%32: every T-table gather is conflict-free.  Address of (x, lane) is
+// perm(x << 8 | (lane & 31) << 2): one v_perm_b32 per lookup.
+constexpr int kLdsWords = 16384;  // 64 KiB
+constexpr int kTableWords = 512;  // A[256], B[256] in global memory
+
+// Workgroup shape of every batch kernel: 8 waves, 2 workgroups per CU.
+constexpr int kThreads = 512;
+constexpr int kWgPerCu = 2;
+// Decrypt: blocks per lane per step (a wave step covers 64*kDecRows blocks).
+constexpr int kDecRows = 4;
+
+struct Fastdiv {  // Lemire: q = mulhi64(M, n) exact for all 32-bit n, d
+    uint64_t M;
+    uint32_t d;
+};
+
+inline Fastdiv make_fastdiv(uint32_t d) {
+    Fastdiv f;
+    f.d = d;
+    f.M = d ? (~0ull / d + 1) : 0;
+    return f;
+}
+
+struct KeySel {
+    const uint32_t* table;     // nkeys * kSchedWords words (device)
+    const uint32_t* key_idx;   // per payload (nullable)
+    Fastdiv ppk;               // payloads per key (d == 0 => key 0)
+    uint32_t nkeys;
+};
+
+struct EncArgs {
+    const uint8_t* in;
+    uint8_t* out;
+    const uint64_t* offsets;  // ragged (nullable => uniform)
+    const uint32_t* nbytes;
+    uint64_t npayloads;
+    uint32_t payload_bytes;
+    KeySel keys;
+    const uint8_t* iv_in;
+    uint8_t* iv_out;
+    const uint32_t* tables;  // TL1[256], TL3[256]
+    uint32_t* status;
+};
+
+struct DecArgs {
+    const uint8_t* in;
+    uint8_t* out;
+    const uint64_t* offsets;  // ragged kernel only
+    const uint32_t* nbytes;
+    uint64_t npayloads;
+    uint64_t nblocks;         // flat kernel: total blocks = npayloads * bpp
+    uint64_t blocks_per_wave; // flat kernel: contiguous range of one wave
+    Fastdiv bpp;              // flat kernel: blocks per payload
+    uint32_t step_q, step_r;  // (64*kDecRows) / bpp, % bpp
+    KeySel keys;
+    const uint8_t* iv_in;
+    uint8_t* iv_out;
+    const uint4* boundary;    // flat kernel in-place: C[begin-1] per wave (nullable)
+    const uint32_t* tables;   // TL5[256], SiW[256]
+    uint32_t* status;
+};
+
+// Launchers (cyaes_kernels.hip).  All asynchronous on `stream`.
+hipError_t launch_encrypt(const EncArgs& a, int grid, hipStream_t stream);
+hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream);
+hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, hipStream_t stream);
+hipError_t launch_boundary_snapshot(const uint8_t* in, uint64_t nblocks, uint64_t blocks_per_wave,
+                                    uint64_t nwaves, Fastdiv bpp, uint4* boundary, hipStream_t stream);
+hipError_t launch_key_expand(const uint8_t* d_keys, uint32_t nkeys, const uint8_t* d_sbox,
+                             uint32_t* d_sched, hipStream_t stream);
+hipError_t launch_fill_synthetic(uint8_t* buf, uint64_t p0, uint64_t npayloads, uint32_t payload_bytes,
+                                 uint64_t seed, hipStream_t stream);
+hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long* out2, hipStream_t stream);
+
+}  // namespace cyaes

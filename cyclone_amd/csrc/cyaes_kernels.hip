@@ -1,0 +1,522 @@
+// cyaes_kernels.hip -- gfx950 (CDNA4) kernels for cyCrypt AES-128-CBC.
+//
+// Reference: thejinchao/cyclone source/cyCrypt/crypt/cyr_rijndael.cpp
+//   encrypt :588-609 (CBC chain) + _encryptBlock :638-705
+//   decrypt :612-635 (CBC chain) + _decryptBlock :708-774
+//
+// Design:
+//  * Cipher state is the block loaded as four little-endian dwords, i.e. the
+//    byte-swap of the reference's big-endian words (cyr_rijndael.cpp:641-656).
+//    Tables and round keys are byte-swapped once on the host, so no swaps run
+//    on the device.
+//  * T-tables live in LDS as a 64 KiB image of 256 rows x 256 B: row x holds
+//    A[x] replicated in 32 slots and B[x] in the next 32.  A lookup address is
+//    one v_perm_b32: (x << 8) | (lane&31)*4; lane l always hits bank l%32, so
+//    the gathers are bank-conflict-free.  The other two T-tables of each
+//    direction are byte rotations (v_alignbit), folded so that encrypt needs
+//    one rotation per column.  The last round's S-box bytes come from the
+//    same rows (encrypt: S[x] is a byte of TL1/TL3; decrypt: B = Si[x]*0x01010101).
+//  * Round keys are wave-uniform and live in SGPRs (s_load from the key table;
+//    a per-payload key index is handled by a waterfall over the distinct keys
+//    present in a wave, normally one).
+//  * Encrypt (serial CBC): one lane = one payload chain, 8 blocks (128 B, one
+//    full line per lane) loaded per step.
+//  * Decrypt (block-parallel): one lane = one 16-B block, each wave-instruction
+//    loads 1 KiB contiguous; the previous ciphertext block comes from the
+//    neighbouring lane through DPP wave_shr:1, the wave's chain across steps is
+//    carried in registers.
+#include "cyaes_internal.h"
+
+namespace cyaes {
+namespace {
+
+constexpr uint32_t kSel0 = 0x0C0C0400u;  // (byte0 of u) << 8 | laneoff
+constexpr uint32_t kSel1 = 0x0C0C0500u;  // (byte1 of u) << 8 | laneoff
+constexpr uint32_t kSel2 = 0x0C0C0600u;
+constexpr uint32_t kSel3 = 0x0C0C0700u;
+constexpr uint32_t kHalfB = 128;         // byte offset of table B inside a row
+constexpr int kWaveShr1 = 0x138;         // DPP wave_shr:1 (lane i <- lane i-1)
+
+// DefaultIV (cyr_rijndael.cpp:503-504) as little-endian dwords.
+constexpr uint32_t kIv0 = 0x03020100u, kIv1 = 0x07060504u, kIv2 = 0x0b0a0908u, kIv3 = 0x0f0e0d0cu;
+
+__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_rotateleft32(x, 8); }
+
+__device__ __forceinline__ uint32_t addr(uint32_t u, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(u, lo, sel);
+}
+
+__device__ __forceinline__ uint32_t ld(const char* lds, uint32_t a) {
+    return *reinterpret_cast<const uint32_t*>(lds + a);
+}
+
+// Fill the 64 KiB LDS image from the two 256-word global tables.
+__device__ __forceinline__ void fill_lds(uint32_t* lds, const uint32_t* __restrict__ tab) {
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+    for (int q = threadIdx.x; q < kLdsWords / 4; q += blockDim.x) {
+        const uint32_t v = tab[((q >> 3) & 1) * 256 + (q >> 4)];
+        l4[q] = make_uint4(v, v, v, v);
+    }
+}
+
+__device__ __forceinline__ uint32_t fastdiv(uint32_t n, const Fastdiv& f) {
+    const uint64_t lo = (uint64_t)(uint32_t)f.M * n;
+    const uint64_t hi = (f.M >> 32) * n;
+    return (uint32_t)((hi + (lo >> 32)) >> 32);
+}
+
+// ---- encryption rounds (_encryptBlock, cyr_rijndael.cpp:659-704) ----------
+// Row layout for encrypt: A = TL1 (bytes 2s,s,s,3s), B = TL3 = rotl16(TL1).
+// TL2 = rotl8(TL1), TL4 = rotl8(TL3), so a column is
+//   TL1[b0(u_j)] ^ TL3[b2(u_j+2)] ^ rotl8(TL1[b1(u_j+1)] ^ TL3[b3(u_j+3)]) ^ k.
+__device__ __forceinline__ uint32_t enc_col(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
+                                            uint32_t x3, uint32_t k) {
+    const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));
+    const uint32_t l1 = ld(lds, addr(x1, lo, kSel1));
+    const uint32_t l2 = ld(lds + kHalfB, addr(x2, lo, kSel2));
+    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, kSel3));
+    return l0 ^ l2 ^ rotl8(l1 ^ l3) ^ k;
+}
+
+// Last round: S[x] sits in byte0/byte3 of TL3 and byte1/byte2 of TL1.
+__device__ __forceinline__ uint32_t enc_last(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
+                                             uint32_t x3, uint32_t k) {
+    const uint32_t l0 = ld(lds + kHalfB, addr(x0, lo, kSel0));
+    const uint32_t l1 = ld(lds, addr(x1, lo, kSel1));
+    const uint32_t l2 = ld(lds, addr(x2, lo, kSel2));
+    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, kSel3));
+    return ((l0 & 0x000000FFu) | (l1 & 0x0000FF00u) | (l2 & 0x00FF0000u) | (l3 & 0xFF000000u)) ^ k;
+}
+
+// s = state already XORed with ek[0..3]; returns ciphertext in s.
+__device__ __forceinline__ void enc_block(const char* lds, uint32_t lo, const uint32_t* __restrict__ ek,
+                                          uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        const uint32_t a0 = enc_col(lds, lo, s0, s1, s2, s3, ek[4 * r + 0]);
+        const uint32_t a1 = enc_col(lds, lo, s1, s2, s3, s0, ek[4 * r + 1]);
+        const uint32_t a2 = enc_col(lds, lo, s2, s3, s0, s1, ek[4 * r + 2]);
+        const uint32_t a3 = enc_col(lds, lo, s3, s0, s1, s2, ek[4 * r + 3]);
+        s0 = a0; s1 = a1; s2 = a2; s3 = a3;
+    }
+    const uint32_t o0 = enc_last(lds, lo, s0, s1, s2, s3, ek[40]);
+    const uint32_t o1 = enc_last(lds, lo, s1, s2, s3, s0, ek[41]);
+    const uint32_t o2 = enc_last(lds, lo, s2, s3, s0, s1, ek[42]);
+    const uint32_t o3 = enc_last(lds, lo, s3, s0, s1, s2, ek[43]);
+    s0 = o0; s1 = o1; s2 = o2; s3 = o3;
+}
+
+// ---- decryption rounds (_decryptBlock, cyr_rijndael.cpp:728-773) ----------
+// Row layout for decrypt: A = TL5 (bytes 14s,9s,13s,11s), B = Si[x]*0x01010101.
+// TL6/7/8 = rotl8/16/24(TL5):  col = L0 ^ rotl8(L1 ^ rotl8(L2 ^ rotl8(L3))) ^ k,
+// with x1 = u_(j-1), x2 = u_(j-2), x3 = u_(j-3) (inverse ShiftRows).
+__device__ __forceinline__ uint32_t dec_col(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
+                                            uint32_t x3, uint32_t k) {
+    const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));
+    const uint32_t l1 = ld(lds, addr(x1, lo, kSel1));
+    const uint32_t l2 = ld(lds, addr(x2, lo, kSel2));
+    const uint32_t l3 = ld(lds, addr(x3, lo, kSel3));
+    return l0 ^ rotl8(l1 ^ rotl8(l2 ^ rotl8(l3))) ^ k;
+}
+
+__device__ __forceinline__ uint32_t dec_last(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
+                                             uint32_t x3, uint32_t k) {
+    const uint32_t l0 = ld(lds + kHalfB, addr(x0, lo, kSel0));
+    const uint32_t l1 = ld(lds + kHalfB, addr(x1, lo, kSel1));
+    const uint32_t l2 = ld(lds + kHalfB, addr(x2, lo, kSel2));
+    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, kSel3));
+    return ((l0 & 0x000000FFu) | (l1 & 0x0000FF00u) | (l2 & 0x00FF0000u) | (l3 & 0xFF000000u)) ^ k;
+}
+
+__device__ __forceinline__ void dec_block(const char* lds, uint32_t lo, const uint32_t* __restrict__ dk,
+                                          uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
+    s0 ^= dk[0]; s1 ^= dk[1]; s2 ^= dk[2]; s3 ^= dk[3];
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        const uint32_t a0 = dec_col(lds, lo, s0, s3, s2, s1, dk[4 * r + 0]);
+        const uint32_t a1 = dec_col(lds, lo, s1, s0, s3, s2, dk[4 * r + 1]);
+        const uint32_t a2 = dec_col(lds, lo, s2, s1, s0, s3, dk[4 * r + 2]);
+        const uint32_t a3 = dec_col(lds, lo, s3, s2, s1, s0, dk[4 * r + 3]);
+        s0 = a0; s1 = a1; s2 = a2; s3 = a3;
+    }
+    const uint32_t o0 = dec_last(lds, lo, s0, s3, s2, s1, dk[40]);
+    const uint32_t o1 = dec_last(lds, lo, s1, s0, s3, s2, dk[41]);
+    const uint32_t o2 = dec_last(lds, lo, s2, s1, s0, s3, dk[42]);
+    const uint32_t o3 = dec_last(lds, lo, s3, s2, s1, s0, dk[43]);
+    s0 = o0; s1 = o1; s2 = o2; s3 = o3;
+}
+
+// Key index of payload p (cyaes.h): key_idx[p] | p / ppk | 0, clamped.
+__device__ __forceinline__ uint32_t key_index(const KeySel& ks, uint64_t p, bool active, uint32_t* status) {
+    if (!active) return 0;
+    uint32_t kid = ks.key_idx ? ks.key_idx[p] : (ks.ppk.d ? fastdiv((uint32_t)p, ks.ppk) : 0u);
+    if (kid >= ks.nkeys) {
+        atomicOr(status, 1u);
+        kid = ks.nkeys - 1;
+    }
+    return kid;
+}
+
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t lane0_value, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0_value, (int)v, kWaveShr1, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ uint32_t rl63(uint32_t v) { return __builtin_amdgcn_readlane(v, 63); }
+
+// ---- CBC encrypt: one lane per payload chain (cyr_rijndael.cpp:588-609) ----
+template <bool RAGGED, bool KEYED>
+__global__ __launch_bounds__(kThreads, 2) void k_encrypt(EncArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsWords];
+    fill_lds(lds_words, a.tables);
+    __syncthreads();
+    const char* lds = reinterpret_cast<const char*>(lds_words);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lo = (threadIdx.x & 31u) << 2;
+    const uint64_t wstride = (uint64_t)gridDim.x * kThreads;
+    const uint64_t wbase0 = (uint64_t)blockIdx.x * kThreads + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+
+    for (uint64_t wbase = wbase0; wbase < a.npayloads; wbase += wstride) {
+        const uint64_t p = wbase + lane;
+        const bool active = p < a.npayloads;
+        uint64_t off;
+        uint32_t nb;
+        if (RAGGED) {
+            off = active ? a.offsets[p] : 0;
+            nb = active ? (a.nbytes[p] >> 4) : 0;
+        } else {
+            off = p * (uint64_t)a.payload_bytes;
+            nb = active ? (a.payload_bytes >> 4) : 0;
+        }
+        const uint32_t kid = KEYED ? key_index(a.keys, p, active, a.status) : 0u;
+        bool pending = active;
+        while (true) {  // waterfall over the distinct keys of this wave
+            const uint64_t m = __ballot(pending);
+            if (m == 0) break;
+            const uint32_t ku = KEYED ? __builtin_amdgcn_readlane(kid, __builtin_ctzll(m)) : 0u;
+            if (pending && (!KEYED || kid == ku)) {
+                pending = false;
+                const uint32_t* __restrict__ ek = a.keys.table + (uint64_t)ku * kSchedWords;
+                uint32_t c0 = kIv0, c1 = kIv1, c2 = kIv2, c3 = kIv3;
+                if (a.iv_in) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(a.iv_in + 16 * p);
+                    c0 = v.x; c1 = v.y; c2 = v.z; c3 = v.w;
+                }
+                const uint4* src = reinterpret_cast<const uint4*>(a.in + off);
+                uint4* dst = reinterpret_cast<uint4*>(a.out + off);
+                uint32_t i = 0;
+                for (; i + 8 <= nb; i += 8) {
+                    uint4 b[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) b[j] = src[i + j];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        c0 ^= b[j].x ^ ek[0]; c1 ^= b[j].y ^ ek[1];
+                        c2 ^= b[j].z ^ ek[2]; c3 ^= b[j].w ^ ek[3];
+                        enc_block(lds, lo, ek, c0, c1, c2, c3);
+                        b[j] = make_uint4(c0, c1, c2, c3);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; j++) dst[i + j] = b[j];
+                }
+                for (; i < nb; i++) {
+                    const uint4 v = src[i];
+                    c0 ^= v.x ^ ek[0]; c1 ^= v.y ^ ek[1]; c2 ^= v.z ^ ek[2]; c3 ^= v.w ^ ek[3];
+                    enc_block(lds, lo, ek, c0, c1, c2, c3);
+                    dst[i] = make_uint4(c0, c1, c2, c3);
+                }
+                if (a.iv_out) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = make_uint4(c0, c1, c2, c3);
+            }
+        }
+    }
+}
+
+// One row of R: decrypt block c (lane's block), given its chain block.
+__device__ __forceinline__ uint4 dec_cbc(const char* lds, uint32_t lo, const uint32_t* __restrict__ dk, uint4 c,
+                                         uint4 prev) {
+    uint32_t s0 = c.x, s1 = c.y, s2 = c.z, s3 = c.w;
+    dec_block(lds, lo, dk, s0, s1, s2, s3);
+    return make_uint4(s0 ^ prev.x, s1 ^ prev.y, s2 ^ prev.z, s3 ^ prev.w);
+}
+
+// ---- CBC decrypt, uniform contiguous batch: one lane per block ------------
+// The batch is one array of nblocks blocks; payload boundaries every bpp
+// blocks restart the chain at the IV.  Each wave owns the contiguous range
+// [w*bpw, (w+1)*bpw) and walks it in steps of 64*R blocks.
+template <bool KEYED>
+__global__ __launch_bounds__(kThreads, 2) void k_decrypt_flat(DecArgs a) {
+    constexpr int R = kDecRows;
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsWords];
+    fill_lds(lds_words, a.tables);
+    __syncthreads();
+    const char* lds = reinterpret_cast<const char*>(lds_words);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lo = (threadIdx.x & 31u) << 2;
+    const uint64_t wave =
+        (uint64_t)blockIdx.x * (kThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t begin = wave * a.blocks_per_wave;
+    if (begin >= a.nblocks) return;
+    const uint64_t end = min(begin + a.blocks_per_wave, a.nblocks);
+    const uint32_t bpp = a.bpp.d;
+    uint64_t bp = begin / bpp;                    // payload of the first block
+    uint32_t bpos = (uint32_t)(begin - bp * bpp); // its position in the payload
+    const uint4* in = reinterpret_cast<const uint4*>(a.in);
+    uint4* out = reinterpret_cast<uint4*>(a.out);
+
+    uint4 carry = make_uint4(0, 0, 0, 0);         // C[begin-1]
+    if (bpos != 0) carry = a.boundary ? a.boundary[wave] : in[begin - 1];
+    const uint32_t* __restrict__ dk0 = a.keys.table + 44;
+
+    for (uint64_t base = begin; base < end; base += 64 * R) {
+        uint4 c[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const uint64_t g = base + 64 * k + lane;
+            c[k] = g < end ? in[g] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const uint64_t g = base + 64 * k + lane;
+            const bool valid = g < end;
+            uint4 prev;
+            prev.x = wave_shr1(k == 0 ? carry.x : rl63(c[k - 1].x), c[k].x);
+            prev.y = wave_shr1(k == 0 ? carry.y : rl63(c[k - 1].y), c[k].y);
+            prev.z = wave_shr1(k == 0 ? carry.z : rl63(c[k - 1].z), c[k].z);
+            prev.w = wave_shr1(k == 0 ? carry.w : rl63(c[k - 1].w), c[k].w);
+            const uint32_t lpos = bpos + 64 * k + lane;
+            const uint32_t q = fastdiv(lpos, a.bpp);
+            const uint32_t r = lpos - q * bpp;
+            const uint64_t p = bp + q;
+            if (r == 0 && valid) {  // first block of a payload: chain = IV
+                prev = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : make_uint4(kIv0, kIv1, kIv2, kIv3);
+            }
+            if (!KEYED) {
+                const uint4 d = dec_cbc(lds, lo, dk0, c[k], prev);
+                if (valid) out[g] = d;
+            } else {
+                const uint32_t kid = key_index(a.keys, p, valid, a.status);
+                bool pending = valid;
+                while (true) {
+                    const uint64_t m = __ballot(pending);
+                    if (m == 0) break;
+                    const uint32_t ku = __builtin_amdgcn_readlane(kid, __builtin_ctzll(m));
+                    if (pending && kid == ku) {
+                        pending = false;
+                        const uint32_t* __restrict__ dk = a.keys.table + (uint64_t)ku * kSchedWords + 44;
+                        out[g] = dec_cbc(lds, lo, dk, c[k], prev);
+                    }
+                }
+            }
+            if (a.iv_out && valid && r == bpp - 1) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+        }
+        carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
+        bpos += a.step_r;
+        bp += a.step_q;
+        if (bpos >= bpp) { bpos -= bpp; bp++; }
+    }
+}
+
+// ---- CBC decrypt, ragged batch: one wave per payload ----------------------
+__global__ __launch_bounds__(kThreads, 2) void k_decrypt_ragged(DecArgs a) {
+    constexpr int R = kDecRows;
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsWords];
+    fill_lds(lds_words, a.tables);
+    __syncthreads();
+    const char* lds = reinterpret_cast<const char*>(lds_words);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lo = (threadIdx.x & 31u) << 2;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kThreads / 64);
+    const uint64_t wave0 =
+        (uint64_t)blockIdx.x * (kThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+    for (uint64_t p = wave0; p < a.npayloads; p += nwaves) {
+        const uint4* in = reinterpret_cast<const uint4*>(a.in + a.offsets[p]);
+        uint4* out = reinterpret_cast<uint4*>(a.out + a.offsets[p]);
+        const uint32_t nb = a.nbytes[p] >> 4;
+        uint32_t kid = a.keys.key_idx ? a.keys.key_idx[p] : (a.keys.ppk.d ? fastdiv((uint32_t)p, a.keys.ppk) : 0u);
+        if (kid >= a.keys.nkeys) {
+            if (lane == 0) atomicOr(a.status, 1u);
+            kid = a.keys.nkeys - 1;
+        }
+        kid = __builtin_amdgcn_readfirstlane(kid);
+        const uint32_t* __restrict__ dk = a.keys.table + (uint64_t)kid * kSchedWords + 44;
+        uint4 carry = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : make_uint4(kIv0, kIv1, kIv2, kIv3);
+        if (nb == 0 && a.iv_out && lane == 0) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = carry;  // chain unchanged
+        for (uint32_t base = 0; base < nb; base += 64 * R) {
+            uint4 c[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const uint32_t g = base + 64 * k + lane;
+                c[k] = g < nb ? in[g] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const uint32_t g = base + 64 * k + lane;
+                uint4 prev;
+                prev.x = wave_shr1(k == 0 ? carry.x : rl63(c[k - 1].x), c[k].x);
+                prev.y = wave_shr1(k == 0 ? carry.y : rl63(c[k - 1].y), c[k].y);
+                prev.z = wave_shr1(k == 0 ? carry.z : rl63(c[k - 1].z), c[k].z);
+                prev.w = wave_shr1(k == 0 ? carry.w : rl63(c[k - 1].w), c[k].w);
+                const uint4 d = dec_cbc(lds, lo, dk, c[k], prev);
+                if (g < nb) out[g] = d;
+                if (a.iv_out && g + 1 == nb) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+            }
+            carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
+        }
+    }
+}
+
+// In-place flat decrypt: snapshot C[begin-1] of every wave range before any
+// wave overwrites it.
+__global__ void k_boundary_snapshot(const uint4* in, uint64_t nblocks, uint64_t bpw, uint64_t nwaves, Fastdiv bpp,
+                                    uint4* boundary) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwaves) return;
+    const uint64_t begin = w * bpw;
+    if (begin == 0 || begin >= nblocks) return;
+    if (begin % bpp.d != 0) boundary[w] = in[begin - 1];
+}
+
+// ---- key schedule (Rijndael::Rijndael, cyr_rijndael.cpp:507-572) ----------
+__device__ __forceinline__ uint32_t xt(uint32_t a) { return ((a << 1) ^ ((a & 0x80u) ? 0x1bu : 0u)) & 0xffu; }
+__device__ __forceinline__ uint32_t gm(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+    for (int i = 0; i < 4; i++) {
+        if (b & (1u << i)) r ^= a;
+        a = xt(a);
+    }
+    return r;
+}
+
+__global__ void k_key_expand(const uint8_t* keys, uint32_t nkeys, const uint8_t* sbox, uint32_t* sched) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nkeys) return;
+    uint32_t w[44];  // big-endian words, reference layout m_Ke
+    for (int j = 0; j < 4; j++) {
+        const uint8_t* k = keys + 16ull * i + 4 * j;
+        w[j] = ((uint32_t)k[0] << 24) | ((uint32_t)k[1] << 16) | ((uint32_t)k[2] << 8) | k[3];
+    }
+    uint32_t rcon = 1;
+    for (int j = 4; j < 44; j++) {
+        uint32_t t = w[j - 1];
+        if ((j & 3) == 0) {
+            t = ((uint32_t)sbox[(t >> 16) & 0xff] << 24) ^ ((uint32_t)sbox[(t >> 8) & 0xff] << 16) ^
+                ((uint32_t)sbox[t & 0xff] << 8) ^ (uint32_t)sbox[t >> 24] ^ (rcon << 24);
+            rcon = xt(rcon);
+        }
+        w[j] = w[j - 4] ^ t;
+    }
+    uint32_t* s = sched + (uint64_t)i * kSchedWords;
+    for (int j = 0; j < 44; j++) s[j] = __builtin_bswap32(w[j]);
+    for (int r = 0; r <= 10; r++) {
+        for (int c = 0; c < 4; c++) {
+            uint32_t t = w[4 * (10 - r) + c];
+            if (r >= 1 && r <= 9) {  // InvMixColumn (cyr_rijndael.cpp:563-571)
+                const uint32_t b0 = t >> 24, b1 = (t >> 16) & 0xff, b2 = (t >> 8) & 0xff, b3 = t & 0xff;
+                t = ((gm(b0, 14) ^ gm(b1, 11) ^ gm(b2, 13) ^ gm(b3, 9)) << 24) |
+                    ((gm(b0, 9) ^ gm(b1, 14) ^ gm(b2, 11) ^ gm(b3, 13)) << 16) |
+                    ((gm(b0, 13) ^ gm(b1, 9) ^ gm(b2, 14) ^ gm(b3, 11)) << 8) |
+                    (gm(b0, 11) ^ gm(b1, 13) ^ gm(b2, 9) ^ gm(b3, 14));
+            }
+            s[44 + 4 * r + c] = __builtin_bswap32(t);
+        }
+    }
+}
+
+// ---- workload utilities --------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void k_fill_synthetic(uint64_t* buf, uint64_t p0, uint64_t npayloads, uint32_t words_pp, uint64_t seed) {
+    const uint64_t total = npayloads * words_pp;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        const uint64_t p = t / words_pp;
+        const uint64_t w = t - p * words_pp;
+        buf[t] = splitmix64(seed + ((p0 + p) << 20) + w);
+    }
+}
+
+__global__ void k_digest(const uint64_t* buf, uint64_t nwords, unsigned long long* out2) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t x = 0, s = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += stride) {
+        const uint64_t h = splitmix64(buf[i] ^ splitmix64(i));
+        x ^= h;
+        s += h;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        x ^= __shfl_xor(x, o);
+        s += __shfl_xor(s, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicXor(&out2[0], (unsigned long long)x);
+        atomicAdd(&out2[1], (unsigned long long)s);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_encrypt(const EncArgs& a, int grid, hipStream_t stream) {
+    const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
+    const bool ragged = a.offsets != nullptr;
+    if (ragged && keyed) hipLaunchKernelGGL((k_encrypt<true, true>), dim3(grid), dim3(kThreads), 0, stream, a);
+    else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false>), dim3(grid), dim3(kThreads), 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_encrypt<false, true>), dim3(grid), dim3(kThreads), 0, stream, a);
+    else hipLaunchKernelGGL((k_encrypt<false, false>), dim3(grid), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream) {
+    const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
+    if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true>), dim3(grid), dim3(kThreads), 0, stream, a);
+    else hipLaunchKernelGGL((k_decrypt_flat<false>), dim3(grid), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL(k_decrypt_ragged, dim3(grid), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_boundary_snapshot(const uint8_t* in, uint64_t nblocks, uint64_t blocks_per_wave, uint64_t nwaves,
+                                    Fastdiv bpp, uint4* boundary, hipStream_t stream) {
+    const int threads = 256;
+    const int grid = (int)((nwaves + threads - 1) / threads);
+    hipLaunchKernelGGL(k_boundary_snapshot, dim3(grid), dim3(threads), 0, stream,
+                       reinterpret_cast<const uint4*>(in), nblocks, blocks_per_wave, nwaves, bpp, boundary);
+    return hipGetLastError();
+}
+
+hipError_t launch_key_expand(const uint8_t* d_keys, uint32_t nkeys, const uint8_t* d_sbox, uint32_t* d_sched,
+                             hipStream_t stream) {
+    const int threads = 64;
+    const int grid = (int)((nkeys + threads - 1) / threads);
+    hipLaunchKernelGGL(k_key_expand, dim3(grid), dim3(threads), 0, stream, d_keys, nkeys, d_sbox, d_sched);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_synthetic(uint8_t* buf, uint64_t p0, uint64_t npayloads, uint32_t payload_bytes, uint64_t seed,
+                                 hipStream_t stream) {
+    const int threads = 256;
+    const uint64_t total = npayloads * (payload_bytes / 8);
+    const uint64_t want = (total + threads - 1) / threads;
+    const int grid = (int)(want < 65536 ? (want ? want : 1) : 65536);
+    hipLaunchKernelGGL(k_fill_synthetic, dim3(grid), dim3(threads), 0, stream, reinterpret_cast<uint64_t*>(buf), p0,
+                       npayloads, payload_bytes / 8, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long* out2, hipStream_t stream) {
+    const int threads = 256;
+    const uint64_t want = (nwords + threads - 1) / threads;
+    const int grid = (int)(want < 8192 ? (want ? want : 1) : 8192);
+    hipLaunchKernelGGL(k_digest, dim3(grid), dim3(threads), 0, stream, reinterpret_cast<const uint64_t*>(buf), nwords,
+                       out2);
+    return hipGetLastError();
+}
+
+}  // namespace cyaes

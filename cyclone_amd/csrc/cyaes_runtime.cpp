@@ -1,0 +1,510 @@
+// cyaes_runtime.cpp -- host runtime behind include/cyaes.h: device context,
+// key table, batch launch geometry, host-memory drop-in path.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+
+#include "cyaes.h"
+#include "cyaes_internal.h"
+#include "cyaes_tables.h"
+
+using namespace cyaes;
+
+struct cyaes_gpu {
+    int device = 0;
+    int num_cus = 0;
+    uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
+    uint32_t* d_keys = nullptr;    // nkeys * kSchedWords
+    uint32_t nkeys = 0;
+    uint32_t key_cap = 0;
+    uint4* d_boundary = nullptr;
+    uint64_t boundary_cap = 0;
+    uint8_t* d_iv_scratch = nullptr;
+    uint64_t iv_cap = 0;
+    uint32_t* d_status = nullptr;
+    unsigned long long* d_digest = nullptr;
+    hipStream_t last_stream = nullptr;
+};
+
+namespace {
+
+constexpr uint64_t kTablesBytes = (512 + 512) * 4 + 256;
+
+int map_err(hipError_t e) {
+    if (e == hipSuccess) return CYAES_OK;
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return CYAES_ENOMEM;
+    return CYAES_EDEVICE;
+}
+
+// Makes ctx->device current for the duration of a call, restoring the
+// caller's device afterwards.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+#define CY_TRY(expr)                         \
+    do {                                     \
+        hipError_t _e = (expr);              \
+        if (_e != hipSuccess) return map_err(_e); \
+    } while (0)
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+template <typename T>
+int ensure(T** buf, uint64_t* cap, uint64_t want_elems) {
+    if (*cap >= want_elems) return CYAES_OK;
+    if (*buf) CY_TRY(hipFree(*buf));
+    *buf = nullptr;
+    *cap = 0;
+    CY_TRY(hipMalloc(reinterpret_cast<void**>(buf), want_elems * sizeof(T)));
+    *cap = want_elems;
+    return CYAES_OK;
+}
+
+// Validates the key-selection arguments of a batch and fills a KeySel.
+int make_keysel(const cyaes_gpu* ctx, uint64_t npayloads, const uint32_t* key_idx, uint32_t ppk, KeySel* ks) {
+    if (ctx->nkeys == 0) return CYAES_ERANGE;
+    if ((key_idx || ppk) && npayloads > 0xFFFFFFFFull) return CYAES_EINVAL;
+    if (!key_idx && ppk && npayloads && (npayloads - 1) / ppk >= ctx->nkeys) return CYAES_ERANGE;
+    ks->table = ctx->d_keys;
+    ks->key_idx = key_idx;
+    ks->ppk = key_idx ? make_fastdiv(0) : make_fastdiv(ppk);
+    ks->nkeys = ctx->nkeys;
+    return CYAES_OK;
+}
+
+int wg_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kWgPerCu); }
+
+int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
+                   uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk,
+                   const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream) {
+    EncArgs a = {};
+    int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys);
+    if (st) return st;
+    a.in = in;
+    a.out = out;
+    a.offsets = offsets;
+    a.nbytes = nbytes;
+    a.npayloads = npayloads;
+    a.payload_bytes = payload_bytes;
+    a.iv_in = iv_in;
+    a.iv_out = iv_out;
+    a.tables = ctx->d_tables;
+    a.status = ctx->d_status;
+    const uint64_t want = (npayloads + kThreads - 1) / kThreads;
+    const int grid = (int)std::min<uint64_t>(want, (uint64_t)wg_cap(ctx));
+    ctx->last_stream = stream;
+    return map_err(launch_encrypt(a, grid, stream));
+}
+
+// d_iv_in == d_iv_out on a block-parallel decrypt: a payload's last block may
+// be written before its first block reads the IV, so read from a copy.
+int alias_iv(cyaes_gpu* ctx, const uint8_t** iv_in, const uint8_t* iv_out, uint64_t npayloads, hipStream_t stream) {
+    if (!*iv_in || *iv_in != iv_out) return CYAES_OK;
+    int st = ensure(&ctx->d_iv_scratch, &ctx->iv_cap, npayloads * 16);
+    if (st) return st;
+    CY_TRY(hipMemcpyAsync(ctx->d_iv_scratch, *iv_in, npayloads * 16, hipMemcpyDeviceToDevice, stream));
+    *iv_in = ctx->d_iv_scratch;
+    return CYAES_OK;
+}
+
+int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t npayloads, uint32_t payload_bytes,
+                    const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream) {
+    DecArgs a = {};
+    int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys);
+    if (st) return st;
+    if ((iv_in || iv_out) && npayloads > 0xFFFFFFFFull) return CYAES_EINVAL;
+    const uint32_t bpp = payload_bytes / 16;
+    const uint64_t nblocks = npayloads * bpp;
+    const uint64_t step = 64ull * kDecRows;
+    const uint64_t waves_needed = (nblocks + step - 1) / step;
+    const int grid = (int)std::min<uint64_t>((waves_needed + 7) / 8, (uint64_t)wg_cap(ctx));
+    const uint64_t nwaves = (uint64_t)grid * (kThreads / 64);
+    uint64_t bpw = (nblocks + nwaves - 1) / nwaves;
+    bpw = (bpw + step - 1) / step * step;
+    st = alias_iv(ctx, &iv_in, iv_out, npayloads, stream);
+    if (st) return st;
+    a.in = in;
+    a.out = out;
+    a.npayloads = npayloads;
+    a.nblocks = nblocks;
+    a.blocks_per_wave = bpw;
+    a.bpp = make_fastdiv(bpp);
+    a.step_q = (uint32_t)(step / bpp);
+    a.step_r = (uint32_t)(step % bpp);
+    a.iv_in = iv_in;
+    a.iv_out = iv_out;
+    a.tables = ctx->d_tables + 512;
+    a.status = ctx->d_status;
+    if (in == out && nwaves > 1) {
+        st = ensure(&ctx->d_boundary, &ctx->boundary_cap, nwaves);
+        if (st) return st;
+        CY_TRY(launch_boundary_snapshot(in, nblocks, bpw, nwaves, a.bpp, ctx->d_boundary, stream));
+        a.boundary = ctx->d_boundary;
+    }
+    ctx->last_stream = stream;
+    return map_err(launch_decrypt_flat(a, grid, stream));
+}
+
+int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
+                   uint64_t npayloads, const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in, uint8_t* iv_out,
+                   hipStream_t stream) {
+    DecArgs a = {};
+    int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys);
+    if (st) return st;
+    st = alias_iv(ctx, &iv_in, iv_out, npayloads, stream);
+    if (st) return st;
+    a.in = in;
+    a.out = out;
+    a.offsets = offsets;
+    a.nbytes = nbytes;
+    a.npayloads = npayloads;
+    a.iv_in = iv_in;
+    a.iv_out = iv_out;
+    a.tables = ctx->d_tables + 512;
+    a.status = ctx->d_status;
+    const int grid = (int)std::min<uint64_t>((npayloads + 7) / 8, (uint64_t)wg_cap(ctx));
+    ctx->last_stream = stream;
+    return map_err(launch_decrypt_ragged(a, grid, stream));
+}
+
+bool batch_args_ok(const cyaes_gpu* ctx, const uint8_t* in, const uint8_t* out, const void* iv_in,
+                   const void* iv_out) {
+    return ctx && in && out && aligned16(in) && aligned16(out) && aligned16(iv_in) && aligned16(iv_out);
+}
+
+}  // namespace
+
+extern "C" {
+
+const uint8_t* cyaes_default_iv(void) {
+    static const uint8_t iv[16] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+    return iv;
+}
+
+const char* cyaes_strerror(int status) {
+    switch (status) {
+        case CYAES_OK: return "ok";
+        case CYAES_EINVAL: return "invalid argument";
+        case CYAES_EDEVICE: return "HIP device error";
+        case CYAES_ENOMEM: return "out of memory";
+        case CYAES_ERANGE: return "key index out of range";
+        case CYAES_ENODEV: return "no gfx950 device";
+        default: return "unknown status";
+    }
+}
+
+const char* cyaes_version(void) { return "cyaes-mi355x 0.1.0 (gfx950, AES-128-CBC, cyclone::Rijndael drop-in)"; }
+
+int cyaes_key_expand(const uint8_t key[16], cyaes_key* out) {
+    if (!key || !out) return CYAES_EINVAL;
+    expand_key(key, out);
+    return CYAES_OK;
+}
+
+int cyaes_gpu_create(int device, cyaes_gpu** out) {
+    if (!out) return CYAES_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return CYAES_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return CYAES_ENODEV;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CYAES_ENODEV;
+    DeviceGuard g(device);
+    if (!g.ok) return CYAES_ENODEV;
+    cyaes_gpu* ctx = new cyaes_gpu();
+    ctx->device = device;
+    ctx->num_cus = prop.multiProcessorCount;
+    const HostTables& t = host_tables();
+    uint8_t host[kTablesBytes];
+    memcpy(host, t.enc, sizeof(t.enc));
+    memcpy(host + 2048, t.dec, sizeof(t.dec));
+    memcpy(host + 4096, t.sbox, 256);
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tables), kTablesBytes);
+    if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, host, kTablesBytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_status), 16);
+    if (e == hipSuccess) e = hipMemset(ctx->d_status, 0, 16);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_digest), 16);
+    if (e != hipSuccess) {
+        cyaes_gpu_destroy(ctx);
+        return map_err(e);
+    }
+    *out = ctx;
+    return CYAES_OK;
+}
+
+void cyaes_gpu_destroy(cyaes_gpu* ctx) {
+    if (!ctx) return;
+    DeviceGuard g(ctx->device);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(ctx->d_tables);
+    (void)hipFree(ctx->d_keys);
+    (void)hipFree(ctx->d_boundary);
+    (void)hipFree(ctx->d_iv_scratch);
+    (void)hipFree(ctx->d_status);
+    (void)hipFree(ctx->d_digest);
+    delete ctx;
+}
+
+int cyaes_gpu_device(const cyaes_gpu* ctx) { return ctx ? ctx->device : -1; }
+int cyaes_gpu_num_cus(const cyaes_gpu* ctx) { return ctx ? ctx->num_cus : 0; }
+uint32_t cyaes_gpu_nkeys(const cyaes_gpu* ctx) { return ctx ? ctx->nkeys : 0; }
+
+static int reserve_keys(cyaes_gpu* ctx, uint32_t nkeys) {
+    if (ctx->key_cap >= nkeys) return CYAES_OK;
+    if (ctx->d_keys) CY_TRY(hipFree(ctx->d_keys));  // hipFree waits for pending work
+    ctx->d_keys = nullptr;
+    ctx->key_cap = 0;
+    CY_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->d_keys), (uint64_t)nkeys * kSchedWords * 4));
+    ctx->key_cap = nkeys;
+    return CYAES_OK;
+}
+
+int cyaes_gpu_set_keys(cyaes_gpu* ctx, const uint8_t* keys, uint32_t nkeys) {
+    if (!ctx || !keys || nkeys == 0) return CYAES_EINVAL;
+    DeviceGuard g(ctx->device);
+    int st = reserve_keys(ctx, nkeys);
+    if (st) return st;
+    uint32_t* host = (uint32_t*)malloc((size_t)nkeys * kSchedWords * 4);
+    if (!host) return CYAES_ENOMEM;
+    for (uint32_t i = 0; i < nkeys; i++) {
+        cyaes_key k;
+        expand_key(keys + 16ull * i, &k);
+        to_device_schedule(k, host + (size_t)i * kSchedWords);
+    }
+    hipError_t e = hipDeviceSynchronize();  // no batch may still read the old table
+    if (e == hipSuccess) e = hipMemcpy(ctx->d_keys, host, (size_t)nkeys * kSchedWords * 4, hipMemcpyHostToDevice);
+    free(host);
+    if (e != hipSuccess) return map_err(e);
+    ctx->nkeys = nkeys;
+    return CYAES_OK;
+}
+
+int cyaes_gpu_set_keys_device(cyaes_gpu* ctx, const uint8_t* d_keys, uint32_t nkeys, void* stream) {
+    if (!ctx || !d_keys || nkeys == 0) return CYAES_EINVAL;
+    DeviceGuard g(ctx->device);
+    int st = reserve_keys(ctx, nkeys);
+    if (st) return st;
+    const uint8_t* d_sbox = reinterpret_cast<const uint8_t*>(ctx->d_tables) + 4096;
+    CY_TRY(launch_key_expand(d_keys, nkeys, d_sbox, ctx->d_keys, (hipStream_t)stream));
+    ctx->nkeys = nkeys;
+    ctx->last_stream = (hipStream_t)stream;
+    return CYAES_OK;
+}
+
+int cyaes_gpu_get_key(cyaes_gpu* ctx, uint32_t index, cyaes_key* out) {
+    if (!ctx || !out) return CYAES_EINVAL;
+    if (index >= ctx->nkeys) return CYAES_ERANGE;
+    DeviceGuard g(ctx->device);
+    uint32_t w[kSchedWords];
+    CY_TRY(hipDeviceSynchronize());
+    CY_TRY(hipMemcpy(w, ctx->d_keys + (uint64_t)index * kSchedWords, sizeof(w), hipMemcpyDeviceToHost));
+    from_device_schedule(w, out);
+    return CYAES_OK;
+}
+
+// Zero-length chains: the final chain is the initial chain (the reference's
+// loop never runs and writes the IV back unchanged, cyr_rijndael.cpp:600-608).
+static int empty_chains(cyaes_gpu* ctx, uint64_t npayloads, const uint32_t* key_idx, uint32_t ppk,
+                        const uint8_t* iv_in, uint8_t* iv_out, void* stream) {
+    if (!iv_out) return CYAES_OK;
+    if (!aligned16(iv_in) || !aligned16(iv_out)) return CYAES_EINVAL;
+    static uint8_t dummy_storage[16] __attribute__((aligned(16)));  // never dereferenced: no blocks
+    DeviceGuard g(ctx->device);
+    return encrypt_common(ctx, dummy_storage, dummy_storage, nullptr, nullptr, npayloads, 0, key_idx, ppk, iv_in,
+                          iv_out, (hipStream_t)stream);
+}
+
+int cyaes_gpu_encrypt_uniform(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, uint64_t npayloads,
+                              uint32_t payload_bytes, const uint32_t* d_key_idx, uint32_t payloads_per_key,
+                              const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream) {
+    if (!ctx || payload_bytes % 16) return CYAES_EINVAL;
+    if (npayloads == 0) return CYAES_OK;
+    if (payload_bytes == 0) return empty_chains(ctx, npayloads, d_key_idx, payloads_per_key, d_iv_in, d_iv_out, stream);
+    if (!batch_args_ok(ctx, d_in, d_out, d_iv_in, d_iv_out)) return CYAES_EINVAL;
+    DeviceGuard g(ctx->device);
+    return encrypt_common(ctx, d_in, d_out, nullptr, nullptr, npayloads, payload_bytes, d_key_idx, payloads_per_key,
+                          d_iv_in, d_iv_out, (hipStream_t)stream);
+}
+
+int cyaes_gpu_decrypt_uniform(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, uint64_t npayloads,
+                              uint32_t payload_bytes, const uint32_t* d_key_idx, uint32_t payloads_per_key,
+                              const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream) {
+    if (!ctx || payload_bytes % 16) return CYAES_EINVAL;
+    if (npayloads == 0) return CYAES_OK;
+    if (payload_bytes == 0) return empty_chains(ctx, npayloads, d_key_idx, payloads_per_key, d_iv_in, d_iv_out, stream);
+    if (!batch_args_ok(ctx, d_in, d_out, d_iv_in, d_iv_out)) return CYAES_EINVAL;
+    DeviceGuard g(ctx->device);
+    return decrypt_uniform(ctx, d_in, d_out, npayloads, payload_bytes, d_key_idx, payloads_per_key, d_iv_in, d_iv_out,
+                           (hipStream_t)stream);
+}
+
+int cyaes_gpu_encrypt_ragged(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, const uint64_t* d_offsets,
+                             const uint32_t* d_nbytes, uint64_t npayloads, const uint32_t* d_key_idx,
+                             uint32_t payloads_per_key, const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream) {
+    if (!ctx) return CYAES_EINVAL;
+    if (npayloads == 0) return CYAES_OK;
+    if (!d_offsets || !d_nbytes || !batch_args_ok(ctx, d_in, d_out, d_iv_in, d_iv_out)) return CYAES_EINVAL;
+    DeviceGuard g(ctx->device);
+    return encrypt_common(ctx, d_in, d_out, d_offsets, d_nbytes, npayloads, 0, d_key_idx, payloads_per_key, d_iv_in,
+                          d_iv_out, (hipStream_t)stream);
+}
+
+int cyaes_gpu_decrypt_ragged(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, const uint64_t* d_offsets,
+                             const uint32_t* d_nbytes, uint64_t npayloads, const uint32_t* d_key_idx,
+                             uint32_t payloads_per_key, const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream) {
+    if (!ctx) return CYAES_EINVAL;
+    if (npayloads == 0) return CYAES_OK;
+    if (!d_offsets || !d_nbytes || !batch_args_ok(ctx, d_in, d_out, d_iv_in, d_iv_out)) return CYAES_EINVAL;
+    DeviceGuard g(ctx->device);
+    return decrypt_ragged(ctx, d_in, d_out, d_offsets, d_nbytes, npayloads, d_key_idx, payloads_per_key, d_iv_in,
+                          d_iv_out, (hipStream_t)stream);
+}
+
+int cyaes_gpu_check(cyaes_gpu* ctx) {
+    if (!ctx) return CYAES_EINVAL;
+    DeviceGuard g(ctx->device);
+    CY_TRY(hipStreamSynchronize(ctx->last_stream));
+    CY_TRY(hipGetLastError());
+    uint32_t status = 0;
+    CY_TRY(hipMemcpy(&status, ctx->d_status, 4, hipMemcpyDeviceToHost));
+    if (status) {
+        CY_TRY(hipMemset(ctx->d_status, 0, 4));
+        return CYAES_ERANGE;
+    }
+    return CYAES_OK;
+}
+
+int cyaes_gpu_fill_synthetic(uint8_t* d_buf, uint64_t p0, uint64_t npayloads, uint32_t payload_bytes, uint64_t seed,
+                             void* stream) {
+    if (!d_buf || payload_bytes % 8) return CYAES_EINVAL;
+    if (npayloads == 0 || payload_bytes == 0) return CYAES_OK;
+    return map_err(launch_fill_synthetic(d_buf, p0, npayloads, payload_bytes, seed, (hipStream_t)stream));
+}
+
+int cyaes_gpu_digest(const uint8_t* d_buf, uint64_t nbytes, uint64_t out[2], void* stream) {
+    if (!out || nbytes % 8 || (nbytes && !d_buf)) return CYAES_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long* d_out = nullptr;
+    CY_TRY(hipMallocAsync(reinterpret_cast<void**>(&d_out), 16, s));
+    hipError_t e = hipMemsetAsync(d_out, 0, 16, s);
+    if (e == hipSuccess && nbytes) e = launch_digest(d_buf, nbytes / 8, d_out, s);
+    unsigned long long h[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d_out, 16, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFreeAsync(d_out, s);
+    if (e != hipSuccess) return map_err(e);
+    out[0] = h[0];
+    out[1] = h[1];
+    return CYAES_OK;
+}
+
+}  // extern "C"
+
+// ---- host-memory drop-in (Rijndael::encrypt / decrypt) --------------------
+namespace {
+
+struct DropIn {
+    std::mutex mu;
+    cyaes_gpu* ctx = nullptr;
+    hipStream_t stream = nullptr;
+    uint8_t* pinned = nullptr;
+    uint64_t pinned_cap = 0;
+    uint8_t* d_buf = nullptr;
+    uint64_t d_cap = 0;
+};
+
+DropIn& dropin() {
+    static DropIn d;
+    return d;
+}
+
+int dropin_ready(DropIn& d, uint64_t size) {
+    if (!d.ctx) {
+        const char* env = getenv("CYAES_DEVICE");
+        int st = cyaes_gpu_create(env ? atoi(env) : 0, &d.ctx);
+        if (st) return st;
+        DeviceGuard g(d.ctx->device);
+        CY_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+        // One key slot: the schedule travels with each call's staging copy.
+        d.ctx->nkeys = 1;
+    }
+    DeviceGuard g(d.ctx->device);
+    const uint64_t need_host = 368 + size;
+    if (d.pinned_cap < need_host) {
+        if (d.pinned) CY_TRY(hipHostFree(d.pinned));
+        d.pinned = nullptr;
+        d.pinned_cap = 0;
+        CY_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.pinned), need_host, hipHostMallocDefault));
+        d.pinned_cap = need_host;
+    }
+    const uint64_t need_dev = need_host + size;
+    if (d.d_cap < need_dev) {
+        if (d.d_buf) CY_TRY(hipFree(d.d_buf));
+        d.d_buf = nullptr;
+        d.d_cap = 0;
+        CY_TRY(hipMalloc(reinterpret_cast<void**>(&d.d_buf), need_dev));
+        d.d_cap = need_dev;
+    }
+    return CYAES_OK;
+}
+
+int dropin_run(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* out, size_t size, uint8_t* iv) {
+    if (!key || !in || !out || size % 16) return CYAES_EINVAL;
+    if (size == 0) return CYAES_OK;  // no-op, IV unchanged (cyr_rijndael.cpp:600 loop never runs)
+    if (size > 0xFFFFFFF0ull) return CYAES_EINVAL;
+    DropIn& d = dropin();
+    std::lock_guard<std::mutex> lock(d.mu);
+    int st = dropin_ready(d, size);
+    if (st) return st;
+    DeviceGuard g(d.ctx->device);
+    // Staging image: [schedule 352 B][chain IV 16 B][payload], one H2D copy.
+    uint32_t* sched = reinterpret_cast<uint32_t*>(d.pinned);
+    to_device_schedule(*key, sched);
+    memcpy(d.pinned + 352, iv ? iv : cyaes_default_iv(), 16);
+    memcpy(d.pinned + 368, in, size);
+    uint8_t final_chain[16];
+    if (decrypt && iv) memcpy(final_chain, in + size - 16, 16);  // before an in-place overwrite
+    const uint64_t image = 368 + size;
+    CY_TRY(hipMemcpyAsync(d.d_buf, d.pinned, image, hipMemcpyHostToDevice, d.stream));
+    cyaes_gpu* ctx = d.ctx;
+    ctx->d_keys = reinterpret_cast<uint32_t*>(d.d_buf);
+    const uint8_t* d_iv = d.d_buf + 352;
+    const uint8_t* d_in = d.d_buf + 368;
+    uint8_t* d_out = d.d_buf + image;
+    st = decrypt ? decrypt_uniform(ctx, d_in, d_out, 1, (uint32_t)size, nullptr, 0, d_iv, nullptr, d.stream)
+                 : encrypt_common(ctx, d_in, d_out, nullptr, nullptr, 1, (uint32_t)size, nullptr, 0, d_iv, nullptr,
+                                  d.stream);
+    ctx->d_keys = nullptr;
+    if (st) return st;
+    CY_TRY(hipMemcpyAsync(d.pinned, d_out, size, hipMemcpyDeviceToHost, d.stream));
+    CY_TRY(hipStreamSynchronize(d.stream));
+    memcpy(out, d.pinned, size);
+    if (iv) memcpy(iv, decrypt ? final_chain : out + size - 16, 16);  // cyr_rijndael.cpp:607-608,633-634
+    return CYAES_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cyaes_cbc_encrypt(const cyaes_key* key, const uint8_t* in, uint8_t* out, size_t size, uint8_t* iv) {
+    return dropin_run(false, key, in, out, size, iv);
+}
+
+int cyaes_cbc_decrypt(const cyaes_key* key, const uint8_t* in, uint8_t* out, size_t size, uint8_t* iv) {
+    return dropin_run(true, key, in, out, size, iv);
+}
+
+}  // extern "C"

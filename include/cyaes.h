@@ -1,0 +1,136 @@
+/*
+ * cyaes.h -- C-ABI of the MI355X-native cyCrypt AES-128-CBC path.
+ *
+ * Drop-in boundary for thejinchao/cyclone `cyclone::Rijndael`
+ * (source/cyCrypt/crypt/cyr_rijndael.h:11-53).  The reference boundary is a
+ * C++ class statically linked into libcyclone.a; this header is the flat
+ * C-ABI beneath the same-shaped C++ class in <cyclone_amd/cyr_rijndael.h>.
+ * Plain pointers and sizes only: no HIP or torch types.  `stream` arguments
+ * are a hipStream_t passed as void* (NULL = the device's null stream).
+ *
+ * Semantics follow the reference exactly:
+ *   - AES-128, CBC mode, no padding; size must be a multiple of 16
+ *     (the reference asserts, cyr_rijndael.cpp:590-591,614-615; here
+ *     CYAES_EINVAL is returned instead).  size == 0 is a no-op.
+ *   - iv == NULL  => chain starts at DefaultIV (cyr_rijndael.cpp:503-504,
+ *     594-598) and nothing is written back.  iv != NULL => chain starts at
+ *     *iv and the final chain block (last ciphertext block) is written back
+ *     (cyr_rijndael.cpp:607-608, 633-634), for encrypt and decrypt alike.
+ *   - in == out (in place) is allowed (cyr_rijndael.cpp:626-629).
+ * Every batch entry point treats each payload as an independent CBC chain,
+ * as the relay sample does (relay_local.cpp:206,365; relay_server.cpp:329,472).
+ */
+#ifndef CYAES_H
+#define CYAES_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CYAES_BLOCK_SIZE 16 /* Rijndael::BLOCK_SIZE, cyr_rijndael.h:14 */
+#define CYAES_ROUNDS 10     /* cyr_rijndael.h:48 */
+
+/* Status codes (the reference has none: it asserts). */
+#define CYAES_OK 0
+#define CYAES_EINVAL (-1)  /* NULL pointer, size % 16 != 0, bad argument   */
+#define CYAES_EDEVICE (-2) /* HIP runtime / launch failure                  */
+#define CYAES_ENOMEM (-3)  /* device or pinned allocation failed            */
+#define CYAES_ERANGE (-4)  /* key index >= number of keys set               */
+#define CYAES_ENODEV (-5)  /* no usable gfx950 device                       */
+
+/* Expanded key: same words and layout as the reference object state
+ * Rijndael::m_Ke / m_Kd (cyr_rijndael.h:48-52; big-endian packed words,
+ * Kd = equivalent inverse cipher schedule). sizeof == 352. */
+typedef struct cyaes_key {
+    uint32_t ke[CYAES_ROUNDS + 1][4];
+    uint32_t kd[CYAES_ROUNDS + 1][4];
+} cyaes_key;
+
+/* Rijndael::DefaultIV, cyr_rijndael.cpp:503-504 (bytes 00 01 .. 0f). */
+const uint8_t* cyaes_default_iv(void);
+const char* cyaes_strerror(int status);
+const char* cyaes_version(void);
+
+/* Rijndael::Rijndael(const BLOCK key), cyr_rijndael.cpp:507-572.
+ * Host-side key schedule (setup, not the hot path). */
+int cyaes_key_expand(const uint8_t key[16], cyaes_key* out);
+
+/* ---- Host-memory drop-in (GPU-executed) -------------------------------
+ * Rijndael::encrypt / Rijndael::decrypt (cyr_rijndael.cpp:588-609, 612-635)
+ * on host buffers.  The call stages through pinned memory, runs the gfx950
+ * kernel on the process default device (env CYAES_DEVICE, default 0) and
+ * returns when the output is in host memory.  Thread-safe (calls serialise
+ * on the process context).  One call = one CBC chain, so encrypt is
+ * latency-bound on any device; batch through the device API for throughput. */
+int cyaes_cbc_encrypt(const cyaes_key* key, const uint8_t* in, uint8_t* out, size_t size, uint8_t* iv);
+int cyaes_cbc_decrypt(const cyaes_key* key, const uint8_t* in, uint8_t* out, size_t size, uint8_t* iv);
+
+/* ---- Device context ----------------------------------------------------- */
+typedef struct cyaes_gpu cyaes_gpu;
+
+int cyaes_gpu_create(int device, cyaes_gpu** out);
+void cyaes_gpu_destroy(cyaes_gpu* ctx);
+int cyaes_gpu_device(const cyaes_gpu* ctx);
+/* Number of compute units, and workgroups the batch kernels launch per CU. */
+int cyaes_gpu_num_cus(const cyaes_gpu* ctx);
+
+/* Session-key table.  set_keys expands nkeys raw 16-byte keys on the host
+ * and uploads the schedules; set_keys_device expands raw keys already in
+ * device memory (e.g. just received by an RCCL broadcast) on the device.
+ * Both replace the whole table.  Synchronous w.r.t. later batch calls on
+ * `stream` (set_keys is fully synchronous). */
+int cyaes_gpu_set_keys(cyaes_gpu* ctx, const uint8_t* keys, uint32_t nkeys);
+int cyaes_gpu_set_keys_device(cyaes_gpu* ctx, const uint8_t* d_keys, uint32_t nkeys, void* stream);
+uint32_t cyaes_gpu_nkeys(const cyaes_gpu* ctx);
+/* Copies schedule `index` back in reference layout (m_Ke/m_Kd). Synchronous. */
+int cyaes_gpu_get_key(cyaes_gpu* ctx, uint32_t index, cyaes_key* out);
+
+/* ---- Device batches (device pointers; asynchronous on `stream`) ---------
+ * Key of payload p:  d_key_idx ? d_key_idx[p]
+ *                  : payloads_per_key ? p / payloads_per_key : 0.
+ * Chain input of payload p:  d_iv_in ? d_iv_in + 16*p : DefaultIV.
+ * If d_iv_out != NULL the final chain block of payload p is written to
+ * d_iv_out + 16*p (d_iv_out may equal d_iv_in).
+ * d_in == d_out (in place) is allowed; partial overlap is undefined.
+ * A d_key_idx entry >= nkeys is clamped and reported by cyaes_gpu_check.
+ *
+ * Uniform layout: payload p occupies bytes [p*payload_bytes, (p+1)*payload_bytes).
+ * Ragged layout:  payload p occupies [d_offsets[p], d_offsets[p] + d_nbytes[p]);
+ *                 offsets and sizes must be multiples of 16. */
+int cyaes_gpu_encrypt_uniform(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, uint64_t npayloads,
+                              uint32_t payload_bytes, const uint32_t* d_key_idx, uint32_t payloads_per_key,
+                              const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream);
+int cyaes_gpu_decrypt_uniform(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, uint64_t npayloads,
+                              uint32_t payload_bytes, const uint32_t* d_key_idx, uint32_t payloads_per_key,
+                              const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream);
+int cyaes_gpu_encrypt_ragged(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, const uint64_t* d_offsets,
+                             const uint32_t* d_nbytes, uint64_t npayloads, const uint32_t* d_key_idx,
+                             uint32_t payloads_per_key, const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream);
+int cyaes_gpu_decrypt_ragged(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, const uint64_t* d_offsets,
+                             const uint32_t* d_nbytes, uint64_t npayloads, const uint32_t* d_key_idx,
+                             uint32_t payloads_per_key, const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream);
+
+/* Synchronises the context's last-used stream and returns CYAES_ERANGE if a
+ * batch since the previous check saw an out-of-range key index (sticky flag
+ * is then cleared), CYAES_EDEVICE on an asynchronous HIP error, else CYAES_OK. */
+int cyaes_gpu_check(cyaes_gpu* ctx);
+
+/* ---- Workload utilities (bench / verification; not on the hot path) ----- */
+/* Synthetic plaintext of SURVEY.md §8(d): 64-bit word w of payload p is
+ * splitmix64(seed + ((p0 + p) << 20) + w), little-endian. payload_bytes % 8 == 0. */
+int cyaes_gpu_fill_synthetic(uint8_t* d_buf, uint64_t p0, uint64_t npayloads, uint32_t payload_bytes,
+                             uint64_t seed, void* stream);
+/* 128-bit order-sensitive digest of nbytes (multiple of 8):
+ *   out[0] = XOR_i h_i,  out[1] = SUM_i h_i (mod 2^64),
+ *   h_i = splitmix64(word_i ^ splitmix64(i)), word_i = i-th LE 64-bit word.
+ * Synchronous (waits on `stream`). */
+int cyaes_gpu_digest(const uint8_t* d_buf, uint64_t nbytes, uint64_t out[2], void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CYAES_H */

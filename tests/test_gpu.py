@@ -1,0 +1,305 @@
+"""GPU parity: the gfx950 HIP path (through the C-ABI) vs the oracle and the
+committed goldens, bit-exact.  Mirrors the reference's Rijndael TEST_CASE
+(thejinchao/cyclone test/unit/cyt_unit_crypt.cpp:173-248) and extends it to
+the batched relay semantics (one chain per payload, relay_local.cpp:206,
+relay_server.cpp:329) at every BASELINE.json config size."""
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import cyclone_amd as ca
+import oracle
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+K0 = oracle.KEY_00_0F
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "gpu tests need a ROCm device"
+    return t
+
+
+@pytest.fixture(scope="module")
+def ctx(torch):
+    c = ca.GpuContext(0)
+    c.set_keys(K0)
+    yield c
+    c.close()
+
+
+def dev(torch, arr):
+    a = np.ascontiguousarray(arr)
+    return torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to("cuda")
+
+
+def host(t):
+    import torch as _t
+    _t.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def empty(torch, n):
+    return torch.empty(max(int(n), 1), dtype=torch.uint8, device="cuda")
+
+
+# ---------------------------------------------------------------- drop-in --
+def test_reference_testcase_cpp(torch):
+    """The C++ re-expression of cyt_unit_crypt.cpp:173-248 against the drop-in class."""
+    subprocess.run(["make", "-C", ROOT, "-s", "cpptest"], check=True)
+    r = subprocess.run([os.path.join(ROOT, "build", "test_rijndael"), os.path.join(ROOT, "tests/golden/ref_kat.txt")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "All tests passed" in r.stdout
+
+
+def test_dropin_python_kat_stream_inplace(golden):
+    k = golden["kat"]
+    aes = ca.Rijndael(bytes.fromhex(k["key"]))
+    plain, cipher = bytes.fromhex(k["plaintext"]), bytes.fromhex(k["ciphertext"])
+    assert bytes(aes.encrypt(plain)) == cipher
+    assert bytes(aes.decrypt(cipher)) == plain
+    for fn, src, want in ((aes.encrypt, plain, cipher), (aes.decrypt, cipher, plain)):
+        iv = bytearray(aes.DefaultIV)
+        out = bytearray()
+        for i in range(0, 64, 16):
+            out += fn(src[i:i + 16], None, 16, iv)
+        assert bytes(out) == want and bytes(iv) == bytes.fromhex(k["iv_check"])
+    buf = bytearray(plain)
+    aes.encrypt(buf, buf)
+    assert bytes(buf) == cipher
+    aes.decrypt(buf, buf)
+    assert bytes(buf) == plain
+
+
+def test_dropin_random_roundtrips():
+    rng = random.Random(3)
+    for _ in range(20):
+        key = bytes(rng.randrange(256) for _ in range(16))
+        data = bytes(rng.randrange(256) for _ in range(128))
+        aes, ref = ca.Rijndael(key), oracle.Rijndael(key)
+        ct = bytes(aes.encrypt(data))
+        assert ct == bytes(ref.encrypt(data))
+        assert bytes(aes.decrypt(ct)) == data
+
+
+def test_dropin_config_sizes(golden):
+    """Single relay-sized calls (up to the 65280 B relay cap and 64 KiB)."""
+    aes = ca.Rijndael(K0)
+    for v in golden["openssl"]["sizes"]:
+        if v["p"]:
+            continue
+        pt = oracle.synthetic(0, 1, v["payload_bytes"]).tobytes()
+        ct = bytes(aes.encrypt(pt))
+        assert ct[-16:].hex() == v["last_block"]
+        assert ct == bytes(oracle.Rijndael(K0).encrypt(pt))
+        assert bytes(aes.decrypt(ct)) == pt
+
+
+# ------------------------------------------------------------- batch API --
+@pytest.mark.parametrize("pb,n", [(16, 5000), (48, 3001), (64, 1000), (1024, 4096), (1472, 2047), (4096, 257),
+                                  (65280, 65), (65536, 96)])
+def test_uniform_batch_vs_oracle(torch, ctx, pb, n):
+    pt = oracle.synthetic(11, n, pb)
+    want = oracle.batch(False, [K0], 0, pt, pb, nthreads=16)
+    d_pt, d_ct, d_rt = dev(torch, pt), empty(torch, pt.size), empty(torch, pt.size)
+    ctx.encrypt_uniform(d_pt, d_ct, n, pb)
+    got = host(d_ct)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, "encrypt mismatch at byte %d (payload %d)" % (bad[0], bad[0] // pb)
+    ctx.decrypt_uniform(d_ct, d_rt, n, pb)
+    assert np.array_equal(host(d_rt), pt)
+    assert ctx.check() == ca.CYAES_OK
+
+
+def test_in_place_batches(torch, ctx):
+    """in == out: encrypt (lane-private) and decrypt (boundary snapshot across waves)."""
+    pb, n = 1472, 30000
+    pt = oracle.synthetic(5, n, pb)
+    want = oracle.batch(False, [K0], 0, pt, pb, nthreads=16)
+    d = dev(torch, pt)
+    ctx.encrypt_uniform(d, d, n, pb)
+    assert np.array_equal(host(d), want)
+    ctx.decrypt_uniform(d, d, n, pb)
+    assert np.array_equal(host(d), pt)
+
+
+def test_session_keys_payloads_per_key(torch, ctx):
+    """Config D shape, scaled: keys grouped by payload (payload p uses key p / ppk)."""
+    nk, ppk, pb = 24, 7, 1472
+    n = nk * ppk
+    keys = [oracle.session_key(s) for s in range(nk)]
+    c = ca.GpuContext(0)
+    c.set_keys(b"".join(keys))
+    pt = oracle.synthetic(0, n, pb)
+    want = oracle.batch(False, keys, ppk, pt, pb, nthreads=16)
+    d_pt, d_ct, d_rt = dev(torch, pt), empty(torch, pt.size), empty(torch, pt.size)
+    c.encrypt_uniform(d_pt, d_ct, n, pb, payloads_per_key=ppk)
+    assert np.array_equal(host(d_ct), want)
+    c.decrypt_uniform(d_ct, d_rt, n, pb, payloads_per_key=ppk)
+    assert np.array_equal(host(d_rt), pt)
+    with pytest.raises(ca.CyaesError):  # (n-1)/ppk >= nkeys
+        c.encrypt_uniform(d_pt, d_ct, n + ppk, pb, payloads_per_key=ppk)
+    c.close()
+
+
+def test_key_index_array_divergent_waves(torch):
+    """Arbitrary per-payload key indices: several keys inside one wave (waterfall)."""
+    rng = np.random.default_rng(9)
+    nk, pb, n = 37, 208, 3000
+    keys = [bytes(rng.integers(0, 256, 16, dtype=np.uint8)) for _ in range(nk)]
+    kidx = rng.integers(0, nk, n, dtype=np.uint32)
+    c = ca.GpuContext(0)
+    c.set_keys(b"".join(keys))
+    pt = oracle.synthetic(3, n, pb)
+    want = np.concatenate([oracle.batch(False, [keys[kidx[p]]], 0, pt[p * pb:(p + 1) * pb], pb) for p in range(n)])
+    d_pt, d_ct, d_rt, d_k = dev(torch, pt), empty(torch, pt.size), empty(torch, pt.size), dev(torch, kidx)
+    c.encrypt_uniform(d_pt, d_ct, n, pb, key_idx=d_k)
+    assert np.array_equal(host(d_ct), want)
+    c.decrypt_uniform(d_ct, d_rt, n, pb, key_idx=d_k)
+    assert np.array_equal(host(d_rt), pt)
+    assert c.check() == ca.CYAES_OK
+    bad = kidx.copy()
+    bad[17] = nk + 3
+    c.encrypt_uniform(d_pt, d_ct, n, pb, key_idx=dev(torch, bad))
+    assert c.check() == ca.CYAES_ERANGE  # reported, then cleared
+    assert c.check() == ca.CYAES_OK
+    c.close()
+
+
+@pytest.mark.parametrize("alias", [False, True])
+def test_iv_in_out(torch, ctx, alias):
+    """Per-payload IV in / final chain out (cyr_rijndael.cpp:594-598, 607-608, 633-634)."""
+    rng = np.random.default_rng(1)
+    pb, n = 1024 + 48, 1500
+    pt = oracle.synthetic(9, n, pb)
+    ivs = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    want_ct, want_iv = np.empty_like(pt), np.empty_like(ivs)
+    for p in range(n):
+        iv = bytearray(ivs[p].tobytes())
+        want_ct[p * pb:(p + 1) * pb] = np.frombuffer(
+            bytes(oracle.Rijndael(K0).encrypt(pt[p * pb:(p + 1) * pb].tobytes(), None, pb, iv)), np.uint8)
+        want_iv[p] = np.frombuffer(bytes(iv), np.uint8)
+    d_pt, d_ct, d_rt = dev(torch, pt), empty(torch, pt.size), empty(torch, pt.size)
+    d_iv = dev(torch, ivs)
+    d_ivo = d_iv if alias else empty(torch, ivs.size)
+    ctx.encrypt_uniform(d_pt, d_ct, n, pb, iv_in=d_iv, iv_out=d_ivo)
+    assert np.array_equal(host(d_ct), want_ct)
+    assert np.array_equal(host(d_ivo).reshape(n, 16), want_iv)
+    d_iv2 = dev(torch, ivs)
+    d_ivo2 = d_iv2 if alias else empty(torch, ivs.size)
+    ctx.decrypt_uniform(d_ct, d_rt, n, pb, iv_in=d_iv2, iv_out=d_ivo2)
+    assert np.array_equal(host(d_rt), pt)
+    assert np.array_equal(host(d_ivo2).reshape(n, 16), want_iv)  # last ciphertext block
+
+
+def test_ragged_batches(torch):
+    """Relay packets of mixed sizes (0..65280 B), gaps between them, per-payload keys and IVs."""
+    rng = np.random.default_rng(4)
+    n = 700
+    sizes = (rng.integers(0, 4081, n) * 16).astype(np.uint32)
+    sizes[:6] = [0, 16, 65280, 1472, 32, 1024]
+    gaps = rng.integers(0, 3, n) * 16
+    offsets = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for p in range(n):
+        pos += int(gaps[p])
+        offsets[p] = pos
+        pos += int(sizes[p])
+    nk = 5
+    keys = [bytes(rng.integers(0, 256, 16, dtype=np.uint8)) for _ in range(nk)]
+    kidx = rng.integers(0, nk, n, dtype=np.uint32)
+    ivs = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    data = rng.integers(0, 256, pos, dtype=np.uint8)
+    want, want_iv = data.copy(), np.empty_like(ivs)
+    for p in range(n):
+        o, s = int(offsets[p]), int(sizes[p])
+        iv = bytearray(ivs[p].tobytes())
+        want[o:o + s] = np.frombuffer(bytes(oracle.Rijndael(keys[kidx[p]]).encrypt(data[o:o + s].tobytes(), None, s, iv)),
+                                      np.uint8)
+        want_iv[p] = np.frombuffer(bytes(iv), np.uint8)
+    c = ca.GpuContext(0)
+    c.set_keys(b"".join(keys))
+    d_in, d_out = dev(torch, data), dev(torch, data)  # gaps keep their bytes
+    d_off, d_nb, d_k = dev(torch, offsets), dev(torch, sizes), dev(torch, kidx)
+    d_iv, d_ivo = dev(torch, ivs), empty(torch, ivs.size)
+    c.encrypt_ragged(d_in, d_out, d_off, d_nb, n, key_idx=d_k, iv_in=d_iv, iv_out=d_ivo)
+    assert np.array_equal(host(d_out), want)
+    assert np.array_equal(host(d_ivo).reshape(n, 16), want_iv)
+    d_back, d_ivo2 = dev(torch, data), empty(torch, ivs.size)
+    c.decrypt_ragged(d_out, d_back, d_off, d_nb, n, key_idx=d_k, iv_in=d_iv, iv_out=d_ivo2)
+    assert np.array_equal(host(d_back), data)
+    got_iv = host(d_ivo2).reshape(n, 16)
+    for p in range(n):
+        o, s = int(offsets[p]), int(sizes[p])
+        exp = want[o + s - 16:o + s] if s else ivs[p]
+        assert np.array_equal(got_iv[p], exp), p
+    c.decrypt_ragged(d_out, d_out, d_off, d_nb, n, key_idx=d_k, iv_in=d_iv)  # in place
+    assert np.array_equal(host(d_out), data)
+    c.close()
+
+
+def test_device_key_expansion(torch):
+    """Keys already on the device (e.g. after the RCCL broadcast) are expanded there."""
+    rng = np.random.default_rng(12)
+    nk = 300
+    raw = rng.integers(0, 256, (nk, 16), dtype=np.uint8)
+    c = ca.GpuContext(0)
+    c.set_keys_device(dev(torch, raw), nk)
+    torch.cuda.synchronize()
+    for i in list(range(5)) + [nk - 1]:
+        assert c.get_key(i).words() == oracle.key_expand(raw[i].tobytes()).words()
+    pb, n = 160, nk
+    pt = oracle.synthetic(0, n, pb)
+    want = np.concatenate([oracle.batch(False, [raw[p].tobytes()], 0, pt[p * pb:(p + 1) * pb], pb) for p in range(n)])
+    d_ct = empty(torch, pt.size)
+    c.encrypt_uniform(dev(torch, pt), d_ct, n, pb, payloads_per_key=1)
+    assert np.array_equal(host(d_ct), want)
+    c.close()
+
+
+def test_fill_and_digest_match_oracle(torch, ctx):
+    pb, n = 1472, 300
+    d = empty(torch, pb * n)
+    ctx.fill_synthetic(d, 77, n, pb, oracle.PLAINTEXT_SEED)
+    want = oracle.synthetic(77, n, pb)
+    assert np.array_equal(host(d), want)
+    assert ctx.digest(d, pb * n) == oracle.digest(want)
+
+
+# ------------------------------------------------- full BASELINE configs --
+@pytest.mark.parametrize("name", ["B", "D", "C", "E_rank1"])
+def test_full_config_digest(torch, golden, name):
+    """Full-size configs on the device vs OpenSSL-derived goldens (checksum of
+    checksums), the round trip, and sampled payloads vs the oracle."""
+    cfg = golden["openssl"]["configs"][name]
+    n, pb, ppk, p0 = cfg["npayloads"], cfg["payload_bytes"], cfg["payloads_per_key"], cfg["p0"]
+    c = ca.GpuContext(0)
+    if ppk:
+        keys = [oracle.session_key(s) for s in range(n // ppk)]
+        c.set_keys(b"".join(keys))
+    else:
+        keys = [K0]
+        c.set_keys(K0)
+    nbytes = n * pb
+    d_pt, d_ct = empty(torch, nbytes), empty(torch, nbytes)
+    c.fill_synthetic(d_pt, p0, n, pb, oracle.PLAINTEXT_SEED)
+    assert ["%016x" % v for v in c.digest(d_pt, nbytes)] == cfg["plain_digest"]
+    c.encrypt_uniform(d_pt, d_ct, n, pb, payloads_per_key=ppk)
+    assert ["%016x" % v for v in c.digest(d_ct, nbytes)] == cfg["cipher_digest"]
+    for p in (0, 1, n // 2 + 3, n - 1):
+        pt = oracle.synthetic(p0 + p, 1, pb)
+        want = oracle.batch(False, [keys[p // ppk] if ppk else K0], 0, pt, pb)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_ct[p * pb:(p + 1) * pb].cpu().numpy(), want), p
+    c.decrypt_uniform(d_ct, d_ct, n, pb, payloads_per_key=ppk)  # in place
+    assert ["%016x" % v for v in c.digest(d_ct, nbytes)] == cfg["plain_digest"]
+    assert c.check() == ca.CYAES_OK
+    del d_pt, d_ct
+    torch.cuda.empty_cache()
+    c.close()

@@ -1,0 +1,148 @@
+"""Pins the oracle (oracle/aes_oracle.c) to the reference before it is trusted.
+
+Reference: thejinchao/cyclone test/unit/cyt_unit_crypt.cpp:173-248 (the
+Rijndael TEST_CASE) and source/cyCrypt/crypt/cyr_rijndael.cpp.  Fixtures:
+tests/golden/ref_kat.json + ref_tables.json (from the reference text by
+gen_ref_fixtures.py) and openssl_vectors.json (gen_openssl_vectors.c).
+"""
+import hashlib
+import random
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+
+
+def test_tables_match_reference_digests(golden):
+    """Regenerated S/Si/T1..T8/U1..U4/rcon == cyr_rijndael.cpp:25-501."""
+    ref = golden["tables"]
+    for name in oracle.TABLE_NAMES:
+        got = oracle.table_bytes(name)
+        assert len(got) == ref[name]["bytes"], name
+        assert hashlib.sha256(got).hexdigest() == ref[name]["sha256"], name
+    assert oracle.default_iv().hex() == ref["DefaultIV"]
+
+
+def test_reference_kat(golden):
+    """cyt_unit_crypt.cpp:190-200: one-shot encrypt / decrypt, iv=nullptr."""
+    k = golden["kat"]
+    aes = oracle.Rijndael(bytes.fromhex(k["key"]))
+    plain, cipher = bytes.fromhex(k["plaintext"]), bytes.fromhex(k["ciphertext"])
+    assert len(plain) % aes.BLOCK_SIZE == 0
+    assert bytes(aes.encrypt(plain)) == cipher
+    assert bytes(aes.decrypt(cipher)) == plain
+
+
+def test_reference_iv_streaming(golden):
+    """cyt_unit_crypt.cpp:203-219: 16-byte calls carrying iv reproduce the chain."""
+    k = golden["kat"]
+    aes = oracle.Rijndael(bytes.fromhex(k["key"]))
+    plain, cipher = bytes.fromhex(k["plaintext"]), bytes.fromhex(k["ciphertext"])
+    iv = bytearray(aes.DefaultIV)
+    out = bytearray()
+    for i in range(0, len(plain), 16):
+        out += aes.encrypt(plain[i:i + 16], None, 16, iv)
+    assert bytes(out) == cipher and bytes(iv) == bytes.fromhex(k["iv_check"])
+    iv = bytearray(aes.DefaultIV)
+    out = bytearray()
+    for i in range(0, len(cipher), 16):
+        out += aes.decrypt(cipher[i:i + 16], None, 16, iv)
+    assert bytes(out) == plain and bytes(iv) == bytes.fromhex(k["iv_check"])
+
+
+def test_reference_in_place(golden):
+    """cyt_unit_crypt.cpp:221-231: encrypt(buf, buf) / decrypt(buf, buf)."""
+    k = golden["kat"]
+    aes = oracle.Rijndael(bytes.fromhex(k["key"]))
+    buf = bytearray.fromhex(k["plaintext"])
+    aes.encrypt(buf, buf)
+    assert buf.hex() == k["ciphertext"]
+    aes.decrypt(buf, buf)
+    assert buf.hex() == k["plaintext"]
+
+
+def test_reference_random_roundtrips():
+    """cyt_unit_crypt.cpp:234-247: 20 random keys, 128-byte round trips."""
+    rng = random.Random(1)
+    for _ in range(20):
+        aes = oracle.Rijndael(bytes(rng.randrange(256) for _ in range(16)))
+        buf = bytes(rng.randrange(256) for _ in range(128))
+        assert bytes(aes.decrypt(aes.encrypt(buf))) == buf
+
+
+def test_size_zero_is_noop_and_bad_size_rejected():
+    aes = oracle.Rijndael(oracle.KEY_00_0F)
+    iv = bytearray(b"\x55" * 16)
+    aes.encrypt(b"", bytearray(16), 0, iv)
+    assert bytes(iv) == b"\x55" * 16
+    with pytest.raises(ValueError):
+        aes.encrypt(b"\0" * 17, bytearray(17), 17)
+
+
+def test_fips197_and_sp800_38a(golden):
+    ov = golden["openssl"]
+    c1 = ov["fips197_c1"]
+    aes = oracle.Rijndael(bytes.fromhex(c1["key"]))
+    assert bytes(aes.encrypt(bytes.fromhex(c1["plaintext"]), None, 16, bytearray(16))).hex() == c1["ciphertext"]
+    f = ov["sp800_38a_f21"]
+    aes = oracle.Rijndael(bytes.fromhex(f["key"]))
+    assert f["iv"] == aes.DefaultIV.hex()  # SP 800-38A's IV is the reference DefaultIV
+    assert bytes(aes.encrypt(bytes.fromhex(f["plaintext"]))).hex() == f["ciphertext"]
+    assert bytes(aes.decrypt(bytes.fromhex(f["ciphertext"]))).hex() == f["plaintext"]  # F.2.2
+
+
+def test_key_schedules_match_openssl(golden):
+    """m_Ke / m_Kd (cyr_rijndael.h:50,52) == OpenSSL rd_key (FIPS-197 A.1 incl.)."""
+    for s in golden["openssl"]["schedules"]:
+        ke, kd = oracle.key_expand(bytes.fromhex(s["key"])).words()
+        assert ke == s["ke"] and kd == s["kd"]
+
+
+def test_synthetic_sizes_match_openssl(golden):
+    """Generator + oracle vs OpenSSL at every configured payload size."""
+    for v in golden["openssl"]["sizes"]:
+        pb, p = v["payload_bytes"], v["p"]
+        pt = oracle.synthetic(p, 1, pb)
+        ct = oracle.batch(False, [oracle.KEY_00_0F], 0, pt, pb)
+        assert hashlib.sha256(ct.tobytes()).hexdigest() == v["cipher_sha256"], (pb, p)
+        assert ct[-16:].tobytes().hex() == v["last_block"]
+        if "ciphertext" in v:
+            assert ct.tobytes().hex() == v["ciphertext"]
+        assert np.array_equal(oracle.batch(True, [oracle.KEY_00_0F], 0, ct, pb), pt)
+
+
+def test_session_keys_match(golden):
+    assert [oracle.session_key(s).hex() for s in range(3)] == golden["openssl"]["session_keys"]
+
+
+def test_config_a_full_digest(golden):
+    """Config A (4096 x 1024 B, the reference's CPU case) end to end on the oracle."""
+    cfg = golden["openssl"]["configs"]["A"]
+    pt = oracle.synthetic(0, cfg["npayloads"], cfg["payload_bytes"])
+    assert "%016x" % oracle.digest(pt)[0] == cfg["plain_digest"][0]
+    ct = oracle.batch(False, [oracle.KEY_00_0F], 0, pt, cfg["payload_bytes"], nthreads=8)
+    x, s = oracle.digest(ct)
+    assert ["%016x" % x, "%016x" % s] == cfg["cipher_digest"]
+    assert np.array_equal(oracle.batch(True, [oracle.KEY_00_0F], 0, ct, cfg["payload_bytes"], nthreads=8), pt)
+
+
+def test_config_d_keyed_prefix(golden):
+    """Config D's per-session keys: first 3 sessions x 256 payloads vs per-payload oracle."""
+    pb, ppk = 1472, 256
+    n = 3 * ppk
+    pt = oracle.synthetic(0, n, pb)
+    keys = [oracle.session_key(s) for s in range(3)]
+    ct = oracle.batch(False, keys, ppk, pt, pb, nthreads=8)
+    for p in (0, 255, 256, 700):
+        one = oracle.Rijndael(keys[p // ppk]).encrypt(pt[p * pb:(p + 1) * pb].tobytes())
+        assert bytes(one) == ct[p * pb:(p + 1) * pb].tobytes()
+
+
+def test_digest_definition():
+    w = np.array([1, 2, 3], dtype="<u8")
+    x, s = oracle.digest(w.view(np.uint8))
+    hs = [int(oracle._splitmix64(np.uint64(v) ^ oracle._splitmix64(np.uint64(i)))) for i, v in enumerate([1, 2, 3])]
+    assert x == hs[0] ^ hs[1] ^ hs[2] and s == sum(hs) % (1 << 64)
+    assert struct.calcsize("<Q") == 8
