@@ -10,22 +10,36 @@ namespace cyaes {
 // Device key schedule: the reference's m_Ke / m_Kd words (cyr_rijndael.h:50,52)
 // byte-swapped to little-endian so a dwordx4 load of a block is directly the
 // cipher state.  88 words = 352 B per key, ek at [0,44), dk at [44,88).
+// Round keys of rounds 1..9 are stored rotated right by 8 bits: the kernels
+// fold the key into the rotated half of each column.
 constexpr int kSchedWords = 88;
 
-// LDS image: 256 rows x 256 B.  Row x holds word A[x] in slots 0..31 and
-// word B[x] in slots 32..63 (one copy per bank), so lane l always reads bank
-// l%32: every T-table gather is conflict-free.  Address of (x, lane) is
-// perm(x << 8 | (lane & 31) << 2): one v_perm_b32 per lookup.
-constexpr int kLdsWords = 16384;  // 64 KiB
-constexpr int kTableWords = 512;  // A[256], B[256] in global memory
+// LDS images.  A row is 256 B: word A[x] in slots 0..31 and
+// word B[x] in slots 32..63, one copy per bank, so lane l always reads bank
+// l%32 and every T-table gather is conflict-free.  The address of (x, lane)
+// is one v_perm_b32: x << 8 | (lane & 31) << 2.
+//   encrypt: one 64 KiB region, A = TL1, B = TL3.
+//   decrypt: region 0 (64 KiB) A = TL5, B = TL7; region 1 (+64 KiB) A = Si x 0x01010101.
+constexpr int kEncLdsWords = 16384;  // 64 KiB
+constexpr int kDecLdsWords = 32768;  // 128 KiB
+constexpr int kEncTableWords = 512;  // TL1[256], TL3[256]
+constexpr int kDecTableWords = 768;  // TL5[256], TL7[256], SiW[256]
+// Byte offsets inside the device table buffer.
+constexpr int kEncTableOff = 0;
+constexpr int kDecTableOff = kEncTableWords * 4;
+constexpr int kSboxOff = kDecTableOff + kDecTableWords * 4;
+constexpr int kTablesBytes = kSboxOff + 256;
 
-// Workgroup shape of every batch kernel: 8 waves, 2 workgroups per CU.
-constexpr int kThreads = 512;
-constexpr int kWgPerCu = 2;
+// Workgroup shapes: encrypt 8 waves x 2 WG/CU (64 KiB LDS each); decrypt
+// 16 waves x 1 WG/CU (128 KiB LDS).  Both give 16 waves per CU.
+constexpr int kEncThreads = 512;
+constexpr int kEncWgPerCu = 2;
+constexpr int kDecThreads = 1024;
+constexpr int kDecWgPerCu = 1;
 // Decrypt: blocks per lane per step (a wave step covers 64*kDecRows blocks).
 constexpr int kDecRows = 4;
 
-struct Fastdiv {  // Lemire: q = mulhi64(M, n) exact for all 32-bit n, d
+struct Fastdiv {  // Lemire: q = mulhi64(M, n) exact for all 32-bit n, d >= 2
     uint64_t M;
     uint32_t d;
 };
@@ -33,7 +47,7 @@ struct Fastdiv {  // Lemire: q = mulhi64(M, n) exact for all 32-bit n, d
 inline Fastdiv make_fastdiv(uint32_t d) {
     Fastdiv f;
     f.d = d;
-    f.M = d ? (~0ull / d + 1) : 0;
+    f.M = d > 1 ? (~0ull / d + 1) : 0;  // d == 1 is special-cased by the device fastdiv
     return f;
 }
 
@@ -54,7 +68,7 @@ struct EncArgs {
     KeySel keys;
     const uint8_t* iv_in;
     uint8_t* iv_out;
-    const uint32_t* tables;  // TL1[256], TL3[256]
+    const uint32_t* tables;  // kEncTableWords
     uint32_t* status;
 };
 
@@ -72,7 +86,8 @@ struct DecArgs {
     const uint8_t* iv_in;
     uint8_t* iv_out;
     const uint4* boundary;    // flat kernel in-place: C[begin-1] per wave (nullable)
-    const uint32_t* tables;   // TL5[256], SiW[256]
+    uint32_t inplace;         // in == out: drain a step's loads before its stores
+    const uint32_t* tables;   // kDecTableWords
     uint32_t* status;
 };
 

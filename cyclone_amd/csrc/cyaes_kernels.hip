@@ -9,38 +9,49 @@
 //    byte-swap of the reference's big-endian words (cyr_rijndael.cpp:641-656).
 //    Tables and round keys are byte-swapped once on the host, so no swaps run
 //    on the device.
-//  * T-tables live in LDS as a 64 KiB image of 256 rows x 256 B: row x holds
-//    A[x] replicated in 32 slots and B[x] in the next 32.  A lookup address is
-//    one v_perm_b32: (x << 8) | (lane&31)*4; lane l always hits bank l%32, so
-//    the gathers are bank-conflict-free.  The other two T-tables of each
-//    direction are byte rotations (v_alignbit), folded so that encrypt needs
-//    one rotation per column.  The last round's S-box bytes come from the
-//    same rows (encrypt: S[x] is a byte of TL1/TL3; decrypt: B = Si[x]*0x01010101).
+//  * T-tables live in LDS as 256 rows x 256 B: row x holds A[x] replicated in
+//    32 slots and B[x] in the next 32.  A lookup address is one v_perm_b32,
+//    (x << 8) | (lane&31)*4, and lane l always hits bank l%32: the gathers are
+//    bank-conflict-free.  Each direction keeps two of its four T-tables
+//    (encrypt TL1/TL3, decrypt TL5/TL7); the other two are rotl8 of those, and
+//    a column needs a single rotation because rotation distributes over XOR:
+//        col = TA[b0] ^ TB[b2] ^ rotl8(TA[b1] ^ TB[b3] ^ rotr8(k)).
+//    The round keys of rounds 1..9 are stored pre-rotated (rotr8(k)), so a
+//    column is xor3, rotate, xor3 (v_bitop3_b32).  The last round's S-box
+//    bytes come from TL1/TL3 bytes (encrypt) or a Si x 0x01010101 region
+//    (decrypt), merged with v_bfi_b32.
 //  * Round keys are wave-uniform and live in SGPRs (s_load from the key table;
 //    a per-payload key index is handled by a waterfall over the distinct keys
 //    present in a wave, normally one).
 //  * Encrypt (serial CBC): one lane = one payload chain, 8 blocks (128 B, one
 //    full line per lane) loaded per step.
 //  * Decrypt (block-parallel): one lane = one 16-B block, each wave-instruction
-//    loads 1 KiB contiguous; the previous ciphertext block comes from the
-//    neighbouring lane through DPP wave_shr:1, the wave's chain across steps is
-//    carried in registers.
+//    loads 1 KiB contiguous; the previous ciphertext block is a second load at
+//    offset -16 (an L1/L2 hit), the wave's chain across steps is carried in
+//    registers.
 #include "cyaes_internal.h"
 
 namespace cyaes {
 namespace {
 
-constexpr uint32_t kSel0 = 0x0C0C0400u;  // (byte0 of u) << 8 | laneoff
-constexpr uint32_t kSel1 = 0x0C0C0500u;  // (byte1 of u) << 8 | laneoff
+// v_perm_b32 selectors: result = (byte k of u) << 8 | lo.byte0 [| lo.byte2 << 16]
+constexpr uint32_t kSel0 = 0x0C0C0400u;
+constexpr uint32_t kSel1 = 0x0C0C0500u;
 constexpr uint32_t kSel2 = 0x0C0C0600u;
 constexpr uint32_t kSel3 = 0x0C0C0700u;
-constexpr uint32_t kHalfB = 128;         // byte offset of table B inside a row
-constexpr int kWaveShr1 = 0x138;         // DPP wave_shr:1 (lane i <- lane i-1)
+// Region-1 selectors: byte2 = 0x02 picks lo.byte2 (= 1), i.e. + 64 KiB.
+constexpr uint32_t region1(uint32_t sel) { return (sel & 0xFF00FFFFu) | 0x00020000u; }
+constexpr uint32_t kHalfB = 128;            // byte offset of table B inside a row
 
 // DefaultIV (cyr_rijndael.cpp:503-504) as little-endian dwords.
 constexpr uint32_t kIv0 = 0x03020100u, kIv1 = 0x07060504u, kIv2 = 0x0b0a0908u, kIv3 = 0x0f0e0d0cu;
 
 __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_rotateleft32(x, 8); }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// (a & m) | (b & ~m): v_bfi_b32
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
 
 __device__ __forceinline__ uint32_t addr(uint32_t u, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(u, lo, sel);
@@ -50,100 +61,103 @@ __device__ __forceinline__ uint32_t ld(const char* lds, uint32_t a) {
     return *reinterpret_cast<const uint32_t*>(lds + a);
 }
 
-// Fill the 64 KiB LDS image from the two 256-word global tables.
-__device__ __forceinline__ void fill_lds(uint32_t* lds, const uint32_t* __restrict__ tab) {
+// Fill an LDS image: nregions x 64 KiB; region r takes A from tab[512r..] and
+// (if has_b[r]) B from tab[512r + 256..].
+__device__ __forceinline__ void fill_region(uint32_t* lds, const uint32_t* __restrict__ a,
+                                            const uint32_t* __restrict__ b, int threads) {
     uint4* l4 = reinterpret_cast<uint4*>(lds);
-    for (int q = threadIdx.x; q < kLdsWords / 4; q += blockDim.x) {
-        const uint32_t v = tab[((q >> 3) & 1) * 256 + (q >> 4)];
+    for (int q = threadIdx.x; q < 4096; q += threads) {
+        const int half = (q >> 3) & 1;
+        if (half && !b) continue;
+        const uint32_t v = (half ? b : a)[q >> 4];
         l4[q] = make_uint4(v, v, v, v);
     }
 }
 
 __device__ __forceinline__ uint32_t fastdiv(uint32_t n, const Fastdiv& f) {
+    if (f.d == 1) return n;  // M = 2^64 does not fit; make_fastdiv leaves 0
     const uint64_t lo = (uint64_t)(uint32_t)f.M * n;
     const uint64_t hi = (f.M >> 32) * n;
     return (uint32_t)((hi + (lo >> 32)) >> 32);
 }
 
-// ---- encryption rounds (_encryptBlock, cyr_rijndael.cpp:659-704) ----------
-// Row layout for encrypt: A = TL1 (bytes 2s,s,s,3s), B = TL3 = rotl16(TL1).
-// TL2 = rotl8(TL1), TL4 = rotl8(TL3), so a column is
-//   TL1[b0(u_j)] ^ TL3[b2(u_j+2)] ^ rotl8(TL1[b1(u_j+1)] ^ TL3[b3(u_j+3)]) ^ k.
-__device__ __forceinline__ uint32_t enc_col(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
-                                            uint32_t x3, uint32_t k) {
+// One middle-round column.  x0..x3 supply bytes b0..b3; A-table reads for
+// b0/b1, B-table reads for b2/b3; kr = rotr8(round key word).
+__device__ __forceinline__ uint32_t col(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
+                                        uint32_t x3, uint32_t kr) {
     const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));
     const uint32_t l1 = ld(lds, addr(x1, lo, kSel1));
     const uint32_t l2 = ld(lds + kHalfB, addr(x2, lo, kSel2));
     const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, kSel3));
-    return l0 ^ l2 ^ rotl8(l1 ^ l3) ^ k;
+    return xor3(l0, l2, rotl8(xor3(l1, l3, kr)));
 }
 
-// Last round: S[x] sits in byte0/byte3 of TL3 and byte1/byte2 of TL1.
+// Merge the four last-round bytes (byte j of word j-th lookup).
+__device__ __forceinline__ uint32_t merge4(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3) {
+    return bfi(0x0000FFFFu, bfi(0x000000FFu, l0, l1), bfi(0x00FF0000u, l2, l3));
+}
+
+// ---- encryption (_encryptBlock, cyr_rijndael.cpp:638-705) -----------------
+// Rows: A = TL1 (LE bytes 2s,s,s,3s), B = TL3 = rotl16(TL1); TL2/TL4 = rotl8.
+// Column j takes b0(u_j), b1(u_j+1), b2(u_j+2), b3(u_j+3) (ShiftRows).
+// Last round: S[x] is byte0/byte3 of TL3 and byte1/byte2 of TL1.
 __device__ __forceinline__ uint32_t enc_last(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
-                                             uint32_t x3, uint32_t k) {
+                                             uint32_t x3) {
     const uint32_t l0 = ld(lds + kHalfB, addr(x0, lo, kSel0));
     const uint32_t l1 = ld(lds, addr(x1, lo, kSel1));
     const uint32_t l2 = ld(lds, addr(x2, lo, kSel2));
     const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, kSel3));
-    return ((l0 & 0x000000FFu) | (l1 & 0x0000FF00u) | (l2 & 0x00FF0000u) | (l3 & 0xFF000000u)) ^ k;
+    return merge4(l0, l1, l2, l3);
 }
 
-// s = state already XORed with ek[0..3]; returns ciphertext in s.
+// s = plaintext ^ chain ^ ek[0..3] on entry, ciphertext on exit.
 __device__ __forceinline__ void enc_block(const char* lds, uint32_t lo, const uint32_t* __restrict__ ek,
                                           uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
 #pragma unroll
     for (int r = 1; r < 10; r++) {
-        const uint32_t a0 = enc_col(lds, lo, s0, s1, s2, s3, ek[4 * r + 0]);
-        const uint32_t a1 = enc_col(lds, lo, s1, s2, s3, s0, ek[4 * r + 1]);
-        const uint32_t a2 = enc_col(lds, lo, s2, s3, s0, s1, ek[4 * r + 2]);
-        const uint32_t a3 = enc_col(lds, lo, s3, s0, s1, s2, ek[4 * r + 3]);
+        const uint32_t a0 = col(lds, lo, s0, s1, s2, s3, ek[4 * r + 0]);
+        const uint32_t a1 = col(lds, lo, s1, s2, s3, s0, ek[4 * r + 1]);
+        const uint32_t a2 = col(lds, lo, s2, s3, s0, s1, ek[4 * r + 2]);
+        const uint32_t a3 = col(lds, lo, s3, s0, s1, s2, ek[4 * r + 3]);
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     }
-    const uint32_t o0 = enc_last(lds, lo, s0, s1, s2, s3, ek[40]);
-    const uint32_t o1 = enc_last(lds, lo, s1, s2, s3, s0, ek[41]);
-    const uint32_t o2 = enc_last(lds, lo, s2, s3, s0, s1, ek[42]);
-    const uint32_t o3 = enc_last(lds, lo, s3, s0, s1, s2, ek[43]);
+    const uint32_t o0 = enc_last(lds, lo, s0, s1, s2, s3) ^ ek[40];
+    const uint32_t o1 = enc_last(lds, lo, s1, s2, s3, s0) ^ ek[41];
+    const uint32_t o2 = enc_last(lds, lo, s2, s3, s0, s1) ^ ek[42];
+    const uint32_t o3 = enc_last(lds, lo, s3, s0, s1, s2) ^ ek[43];
     s0 = o0; s1 = o1; s2 = o2; s3 = o3;
 }
 
-// ---- decryption rounds (_decryptBlock, cyr_rijndael.cpp:728-773) ----------
-// Row layout for decrypt: A = TL5 (bytes 14s,9s,13s,11s), B = Si[x]*0x01010101.
-// TL6/7/8 = rotl8/16/24(TL5):  col = L0 ^ rotl8(L1 ^ rotl8(L2 ^ rotl8(L3))) ^ k,
-// with x1 = u_(j-1), x2 = u_(j-2), x3 = u_(j-3) (inverse ShiftRows).
-__device__ __forceinline__ uint32_t dec_col(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
-                                            uint32_t x3, uint32_t k) {
-    const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));
-    const uint32_t l1 = ld(lds, addr(x1, lo, kSel1));
-    const uint32_t l2 = ld(lds, addr(x2, lo, kSel2));
-    const uint32_t l3 = ld(lds, addr(x3, lo, kSel3));
-    return l0 ^ rotl8(l1 ^ rotl8(l2 ^ rotl8(l3))) ^ k;
-}
-
+// ---- decryption (_decryptBlock, cyr_rijndael.cpp:708-774) -----------------
+// Region 0 rows: A = TL5 (LE bytes 14s,9s,13s,11s), B = TL7 = rotl16(TL5);
+// TL6/TL8 = rotl8.  Column j takes b0(u_j), b1(u_j-1), b2(u_j-2), b3(u_j-3)
+// (inverse ShiftRows, cyr_rijndael.cpp:731-746).  Region 1 rows: A = Si[x]
+// in all four bytes, addressed through lo.byte2 = 1 (region1()).
 __device__ __forceinline__ uint32_t dec_last(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
-                                             uint32_t x3, uint32_t k) {
-    const uint32_t l0 = ld(lds + kHalfB, addr(x0, lo, kSel0));
-    const uint32_t l1 = ld(lds + kHalfB, addr(x1, lo, kSel1));
-    const uint32_t l2 = ld(lds + kHalfB, addr(x2, lo, kSel2));
-    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, kSel3));
-    return ((l0 & 0x000000FFu) | (l1 & 0x0000FF00u) | (l2 & 0x00FF0000u) | (l3 & 0xFF000000u)) ^ k;
+                                             uint32_t x3) {
+    const uint32_t l0 = ld(lds, addr(x0, lo, region1(kSel0)));
+    const uint32_t l1 = ld(lds, addr(x1, lo, region1(kSel1)));
+    const uint32_t l2 = ld(lds, addr(x2, lo, region1(kSel2)));
+    const uint32_t l3 = ld(lds, addr(x3, lo, region1(kSel3)));
+    return merge4(l0, l1, l2, l3);
 }
 
-__device__ __forceinline__ void dec_block(const char* lds, uint32_t lo, const uint32_t* __restrict__ dk,
-                                          uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
-    s0 ^= dk[0]; s1 ^= dk[1]; s2 ^= dk[2]; s3 ^= dk[3];
+// Returns D(c) ^ prev (CBC, cyr_rijndael.cpp:625-630).
+__device__ __forceinline__ uint4 dec_cbc(const char* lds, uint32_t lo, const uint32_t* __restrict__ dk, uint4 c,
+                                         uint4 prev) {
+    uint32_t s0 = c.x ^ dk[0], s1 = c.y ^ dk[1], s2 = c.z ^ dk[2], s3 = c.w ^ dk[3];
 #pragma unroll
     for (int r = 1; r < 10; r++) {
-        const uint32_t a0 = dec_col(lds, lo, s0, s3, s2, s1, dk[4 * r + 0]);
-        const uint32_t a1 = dec_col(lds, lo, s1, s0, s3, s2, dk[4 * r + 1]);
-        const uint32_t a2 = dec_col(lds, lo, s2, s1, s0, s3, dk[4 * r + 2]);
-        const uint32_t a3 = dec_col(lds, lo, s3, s2, s1, s0, dk[4 * r + 3]);
+        const uint32_t a0 = col(lds, lo, s0, s3, s2, s1, dk[4 * r + 0]);
+        const uint32_t a1 = col(lds, lo, s1, s0, s3, s2, dk[4 * r + 1]);
+        const uint32_t a2 = col(lds, lo, s2, s1, s0, s3, dk[4 * r + 2]);
+        const uint32_t a3 = col(lds, lo, s3, s2, s1, s0, dk[4 * r + 3]);
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     }
-    const uint32_t o0 = dec_last(lds, lo, s0, s3, s2, s1, dk[40]);
-    const uint32_t o1 = dec_last(lds, lo, s1, s0, s3, s2, dk[41]);
-    const uint32_t o2 = dec_last(lds, lo, s2, s1, s0, s3, dk[42]);
-    const uint32_t o3 = dec_last(lds, lo, s3, s2, s1, s0, dk[43]);
-    s0 = o0; s1 = o1; s2 = o2; s3 = o3;
+    return make_uint4(xor3(dec_last(lds, lo, s0, s3, s2, s1), dk[40], prev.x),
+                      xor3(dec_last(lds, lo, s1, s0, s3, s2), dk[41], prev.y),
+                      xor3(dec_last(lds, lo, s2, s1, s0, s3), dk[42], prev.z),
+                      xor3(dec_last(lds, lo, s3, s2, s1, s0), dk[43], prev.w));
 }
 
 // Key index of payload p (cyaes.h): key_idx[p] | p / ppk | 0, clamped.
@@ -157,23 +171,25 @@ __device__ __forceinline__ uint32_t key_index(const KeySel& ks, uint64_t p, bool
     return kid;
 }
 
-__device__ __forceinline__ uint32_t wave_shr1(uint32_t lane0_value, uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0_value, (int)v, kWaveShr1, 0xf, 0xf, false);
-}
-
 __device__ __forceinline__ uint32_t rl63(uint32_t v) { return __builtin_amdgcn_readlane(v, 63); }
+
+__device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kIv2, kIv3); }
+
+// In-place batches: every load of a step must have returned before the step's
+// first store (a lane's previous-block load reads a neighbour's block).
+__device__ __forceinline__ void drain_loads() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---- CBC encrypt: one lane per payload chain (cyr_rijndael.cpp:588-609) ----
 template <bool RAGGED, bool KEYED>
-__global__ __launch_bounds__(kThreads, 2) void k_encrypt(EncArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsWords];
-    fill_lds(lds_words, a.tables);
+__global__ __launch_bounds__(kEncThreads, 2) void k_encrypt(EncArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
+    fill_region(lds_words, a.tables, a.tables + 256, kEncThreads);
     __syncthreads();
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lo = (threadIdx.x & 31u) << 2;
-    const uint64_t wstride = (uint64_t)gridDim.x * kThreads;
-    const uint64_t wbase0 = (uint64_t)blockIdx.x * kThreads + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+    const uint64_t wstride = (uint64_t)gridDim.x * kEncThreads;
+    const uint64_t wbase0 = (uint64_t)blockIdx.x * kEncThreads + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
 
     for (uint64_t wbase = wbase0; wbase < a.npayloads; wbase += wstride) {
         const uint64_t p = wbase + lane;
@@ -196,11 +212,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_encrypt(EncArgs a) {
             if (pending && (!KEYED || kid == ku)) {
                 pending = false;
                 const uint32_t* __restrict__ ek = a.keys.table + (uint64_t)ku * kSchedWords;
-                uint32_t c0 = kIv0, c1 = kIv1, c2 = kIv2, c3 = kIv3;
-                if (a.iv_in) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(a.iv_in + 16 * p);
-                    c0 = v.x; c1 = v.y; c2 = v.z; c3 = v.w;
-                }
+                uint4 c = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
                 const uint4* src = reinterpret_cast<const uint4*>(a.in + off);
                 uint4* dst = reinterpret_cast<uint4*>(a.out + off);
                 uint32_t i = 0;
@@ -210,85 +222,87 @@ __global__ __launch_bounds__(kThreads, 2) void k_encrypt(EncArgs a) {
                     for (int j = 0; j < 8; j++) b[j] = src[i + j];
 #pragma unroll
                     for (int j = 0; j < 8; j++) {
-                        c0 ^= b[j].x ^ ek[0]; c1 ^= b[j].y ^ ek[1];
-                        c2 ^= b[j].z ^ ek[2]; c3 ^= b[j].w ^ ek[3];
-                        enc_block(lds, lo, ek, c0, c1, c2, c3);
-                        b[j] = make_uint4(c0, c1, c2, c3);
+                        uint32_t s0 = xor3(c.x, b[j].x, ek[0]), s1 = xor3(c.y, b[j].y, ek[1]);
+                        uint32_t s2 = xor3(c.z, b[j].z, ek[2]), s3 = xor3(c.w, b[j].w, ek[3]);
+                        enc_block(lds, lo, ek, s0, s1, s2, s3);
+                        c = make_uint4(s0, s1, s2, s3);
+                        b[j] = c;
                     }
 #pragma unroll
                     for (int j = 0; j < 8; j++) dst[i + j] = b[j];
                 }
                 for (; i < nb; i++) {
                     const uint4 v = src[i];
-                    c0 ^= v.x ^ ek[0]; c1 ^= v.y ^ ek[1]; c2 ^= v.z ^ ek[2]; c3 ^= v.w ^ ek[3];
-                    enc_block(lds, lo, ek, c0, c1, c2, c3);
-                    dst[i] = make_uint4(c0, c1, c2, c3);
+                    uint32_t s0 = xor3(c.x, v.x, ek[0]), s1 = xor3(c.y, v.y, ek[1]);
+                    uint32_t s2 = xor3(c.z, v.z, ek[2]), s3 = xor3(c.w, v.w, ek[3]);
+                    enc_block(lds, lo, ek, s0, s1, s2, s3);
+                    c = make_uint4(s0, s1, s2, s3);
+                    dst[i] = c;
                 }
-                if (a.iv_out) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = make_uint4(c0, c1, c2, c3);
+                if (a.iv_out) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c;
             }
         }
     }
 }
 
-// One row of R: decrypt block c (lane's block), given its chain block.
-__device__ __forceinline__ uint4 dec_cbc(const char* lds, uint32_t lo, const uint32_t* __restrict__ dk, uint4 c,
-                                         uint4 prev) {
-    uint32_t s0 = c.x, s1 = c.y, s2 = c.z, s3 = c.w;
-    dec_block(lds, lo, dk, s0, s1, s2, s3);
-    return make_uint4(s0 ^ prev.x, s1 ^ prev.y, s2 ^ prev.z, s3 ^ prev.w);
-}
-
 // ---- CBC decrypt, uniform contiguous batch: one lane per block ------------
 // The batch is one array of nblocks blocks; payload boundaries every bpp
 // blocks restart the chain at the IV.  Each wave owns the contiguous range
-// [w*bpw, (w+1)*bpw) and walks it in steps of 64*R blocks.
-template <bool KEYED>
-__global__ __launch_bounds__(kThreads, 2) void k_decrypt_flat(DecArgs a) {
+// [w*bpw, (w+1)*bpw) and walks it in steps of 64*R blocks.  BIG: bpp >= 64*R,
+// so a step crosses at most one payload boundary and no division is needed.
+template <bool KEYED, bool BIG>
+__global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     constexpr int R = kDecRows;
-    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsWords];
-    fill_lds(lds_words, a.tables);
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
+    fill_region(lds_words, a.tables, a.tables + 256, kDecThreads);
+    fill_region(lds_words + 16384, a.tables + 512, nullptr, kDecThreads);
     __syncthreads();
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lo = (threadIdx.x & 31u) << 2;
+    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
     const uint64_t wave =
-        (uint64_t)blockIdx.x * (kThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t begin = wave * a.blocks_per_wave;
     if (begin >= a.nblocks) return;
     const uint64_t end = min(begin + a.blocks_per_wave, a.nblocks);
     const uint32_t bpp = a.bpp.d;
-    uint64_t bp = begin / bpp;                    // payload of the first block
+    uint64_t bp = begin / bpp;                    // payload of the step's first block
     uint32_t bpos = (uint32_t)(begin - bp * bpp); // its position in the payload
     const uint4* in = reinterpret_cast<const uint4*>(a.in);
     uint4* out = reinterpret_cast<uint4*>(a.out);
+    const bool inplace = a.inplace != 0;
 
     uint4 carry = make_uint4(0, 0, 0, 0);         // C[begin-1]
     if (bpos != 0) carry = a.boundary ? a.boundary[wave] : in[begin - 1];
     const uint32_t* __restrict__ dk0 = a.keys.table + 44;
 
     for (uint64_t base = begin; base < end; base += 64 * R) {
-        uint4 c[R];
-#pragma unroll
-        for (int k = 0; k < R; k++) {
-            const uint64_t g = base + 64 * k + lane;
-            c[k] = g < end ? in[g] : make_uint4(0, 0, 0, 0);
-        }
+        uint4 c[R], pv[R];
 #pragma unroll
         for (int k = 0; k < R; k++) {
             const uint64_t g = base + 64 * k + lane;
             const bool valid = g < end;
-            uint4 prev;
-            prev.x = wave_shr1(k == 0 ? carry.x : rl63(c[k - 1].x), c[k].x);
-            prev.y = wave_shr1(k == 0 ? carry.y : rl63(c[k - 1].y), c[k].y);
-            prev.z = wave_shr1(k == 0 ? carry.z : rl63(c[k - 1].z), c[k].z);
-            prev.w = wave_shr1(k == 0 ? carry.w : rl63(c[k - 1].w), c[k].w);
+            c[k] = valid ? in[g] : make_uint4(0, 0, 0, 0);
+            pv[k] = (valid && (k > 0 || lane > 0)) ? in[g - 1] : carry;
+        }
+        if (inplace) drain_loads();
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const uint64_t g = base + 64 * k + lane;
+            const bool valid = g < end;
             const uint32_t lpos = bpos + 64 * k + lane;
-            const uint32_t q = fastdiv(lpos, a.bpp);
-            const uint32_t r = lpos - q * bpp;
-            const uint64_t p = bp + q;
-            if (r == 0 && valid) {  // first block of a payload: chain = IV
-                prev = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : make_uint4(kIv0, kIv1, kIv2, kIv3);
+            uint32_t r;
+            uint64_t p;
+            if (BIG) {
+                r = min(lpos, lpos - bpp);
+                p = bp + (lpos >= bpp ? 1 : 0);
+            } else {
+                const uint32_t q = fastdiv(lpos, a.bpp);
+                r = lpos - q * bpp;
+                p = bp + q;
             }
+            uint4 prev = pv[k];
+            if (r == 0) prev = (a.iv_in && valid) ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
             if (!KEYED) {
                 const uint4 d = dec_cbc(lds, lo, dk0, c[k], prev);
                 if (valid) out[g] = d;
@@ -316,17 +330,19 @@ __global__ __launch_bounds__(kThreads, 2) void k_decrypt_flat(DecArgs a) {
 }
 
 // ---- CBC decrypt, ragged batch: one wave per payload ----------------------
-__global__ __launch_bounds__(kThreads, 2) void k_decrypt_ragged(DecArgs a) {
+__global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     constexpr int R = kDecRows;
-    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsWords];
-    fill_lds(lds_words, a.tables);
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
+    fill_region(lds_words, a.tables, a.tables + 256, kDecThreads);
+    fill_region(lds_words + 16384, a.tables + 512, nullptr, kDecThreads);
     __syncthreads();
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lo = (threadIdx.x & 31u) << 2;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kThreads / 64);
+    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kDecThreads / 64);
     const uint64_t wave0 =
-        (uint64_t)blockIdx.x * (kThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool inplace = a.inplace != 0;
 
     for (uint64_t p = wave0; p < a.npayloads; p += nwaves) {
         const uint4* in = reinterpret_cast<const uint4*>(a.in + a.offsets[p]);
@@ -339,24 +355,22 @@ __global__ __launch_bounds__(kThreads, 2) void k_decrypt_ragged(DecArgs a) {
         }
         kid = __builtin_amdgcn_readfirstlane(kid);
         const uint32_t* __restrict__ dk = a.keys.table + (uint64_t)kid * kSchedWords + 44;
-        uint4 carry = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : make_uint4(kIv0, kIv1, kIv2, kIv3);
+        uint4 carry = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
         if (nb == 0 && a.iv_out && lane == 0) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = carry;  // chain unchanged
         for (uint32_t base = 0; base < nb; base += 64 * R) {
-            uint4 c[R];
+            uint4 c[R], pv[R];
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 const uint32_t g = base + 64 * k + lane;
-                c[k] = g < nb ? in[g] : make_uint4(0, 0, 0, 0);
+                const bool valid = g < nb;
+                c[k] = valid ? in[g] : make_uint4(0, 0, 0, 0);
+                pv[k] = (valid && (k > 0 || lane > 0)) ? in[g - 1] : carry;
             }
+            if (inplace) drain_loads();
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 const uint32_t g = base + 64 * k + lane;
-                uint4 prev;
-                prev.x = wave_shr1(k == 0 ? carry.x : rl63(c[k - 1].x), c[k].x);
-                prev.y = wave_shr1(k == 0 ? carry.y : rl63(c[k - 1].y), c[k].y);
-                prev.z = wave_shr1(k == 0 ? carry.z : rl63(c[k - 1].z), c[k].z);
-                prev.w = wave_shr1(k == 0 ? carry.w : rl63(c[k - 1].w), c[k].w);
-                const uint4 d = dec_cbc(lds, lo, dk, c[k], prev);
+                const uint4 d = dec_cbc(lds, lo, dk, c[k], pv[k]);
                 if (g < nb) out[g] = d;
                 if (a.iv_out && g + 1 == nb) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
             }
@@ -405,8 +419,12 @@ __global__ void k_key_expand(const uint8_t* keys, uint32_t nkeys, const uint8_t*
         }
         w[j] = w[j - 4] ^ t;
     }
+    // Device layout (cyaes_internal.h): LE words, rounds 1..9 rotated right by 8.
     uint32_t* s = sched + (uint64_t)i * kSchedWords;
-    for (int j = 0; j < 44; j++) s[j] = __builtin_bswap32(w[j]);
+    for (int j = 0; j < 44; j++) {
+        const uint32_t v = __builtin_bswap32(w[j]);
+        s[j] = (j >= 4 && j < 40) ? __builtin_rotateright32(v, 8) : v;
+    }
     for (int r = 0; r <= 10; r++) {
         for (int c = 0; c < 4; c++) {
             uint32_t t = w[4 * (10 - r) + c];
@@ -417,7 +435,8 @@ __global__ void k_key_expand(const uint8_t* keys, uint32_t nkeys, const uint8_t*
                     ((gm(b0, 13) ^ gm(b1, 9) ^ gm(b2, 14) ^ gm(b3, 11)) << 8) |
                     (gm(b0, 11) ^ gm(b1, 13) ^ gm(b2, 9) ^ gm(b3, 14));
             }
-            s[44 + 4 * r + c] = __builtin_bswap32(t);
+            const uint32_t v = __builtin_bswap32(t);
+            s[44 + 4 * r + c] = (r >= 1 && r <= 9) ? __builtin_rotateright32(v, 8) : v;
         }
     }
 }
@@ -463,22 +482,27 @@ __global__ void k_digest(const uint64_t* buf, uint64_t nwords, unsigned long lon
 hipError_t launch_encrypt(const EncArgs& a, int grid, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
     const bool ragged = a.offsets != nullptr;
-    if (ragged && keyed) hipLaunchKernelGGL((k_encrypt<true, true>), dim3(grid), dim3(kThreads), 0, stream, a);
-    else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false>), dim3(grid), dim3(kThreads), 0, stream, a);
-    else if (keyed) hipLaunchKernelGGL((k_encrypt<false, true>), dim3(grid), dim3(kThreads), 0, stream, a);
-    else hipLaunchKernelGGL((k_encrypt<false, false>), dim3(grid), dim3(kThreads), 0, stream, a);
+    const dim3 g(grid), b(kEncThreads);
+    if (ragged && keyed) hipLaunchKernelGGL((k_encrypt<true, true>), g, b, 0, stream, a);
+    else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false>), g, b, 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_encrypt<false, true>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((k_encrypt<false, false>), g, b, 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
-    if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true>), dim3(grid), dim3(kThreads), 0, stream, a);
-    else hipLaunchKernelGGL((k_decrypt_flat<false>), dim3(grid), dim3(kThreads), 0, stream, a);
+    const bool big = a.bpp.d >= 64u * kDecRows;
+    const dim3 g(grid), b(kDecThreads);
+    if (keyed && big) hipLaunchKernelGGL((k_decrypt_flat<true, true>), g, b, 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true, false>), g, b, 0, stream, a);
+    else if (big) hipLaunchKernelGGL((k_decrypt_flat<false, true>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((k_decrypt_flat<false, false>), g, b, 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, hipStream_t stream) {
-    hipLaunchKernelGGL(k_decrypt_ragged, dim3(grid), dim3(kThreads), 0, stream, a);
+    hipLaunchKernelGGL(k_decrypt_ragged, dim3(grid), dim3(kDecThreads), 0, stream, a);
     return hipGetLastError();
 }
 

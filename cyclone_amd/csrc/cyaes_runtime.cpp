@@ -31,7 +31,6 @@ struct cyaes_gpu {
 
 namespace {
 
-constexpr uint64_t kTablesBytes = (512 + 512) * 4 + 256;
 
 int map_err(hipError_t e) {
     if (e == hipSuccess) return CYAES_OK;
@@ -84,7 +83,8 @@ int make_keysel(const cyaes_gpu* ctx, uint64_t npayloads, const uint32_t* key_id
     return CYAES_OK;
 }
 
-int wg_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kWgPerCu); }
+int enc_grid_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kEncWgPerCu); }
+int dec_grid_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kDecWgPerCu); }
 
 int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
                    uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk,
@@ -100,10 +100,10 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.payload_bytes = payload_bytes;
     a.iv_in = iv_in;
     a.iv_out = iv_out;
-    a.tables = ctx->d_tables;
+    a.tables = ctx->d_tables + kEncTableOff / 4;
     a.status = ctx->d_status;
-    const uint64_t want = (npayloads + kThreads - 1) / kThreads;
-    const int grid = (int)std::min<uint64_t>(want, (uint64_t)wg_cap(ctx));
+    const uint64_t want = (npayloads + kEncThreads - 1) / kEncThreads;
+    const int grid = (int)std::min<uint64_t>(want, (uint64_t)enc_grid_cap(ctx));
     ctx->last_stream = stream;
     return map_err(launch_encrypt(a, grid, stream));
 }
@@ -129,8 +129,9 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     const uint64_t nblocks = npayloads * bpp;
     const uint64_t step = 64ull * kDecRows;
     const uint64_t waves_needed = (nblocks + step - 1) / step;
-    const int grid = (int)std::min<uint64_t>((waves_needed + 7) / 8, (uint64_t)wg_cap(ctx));
-    const uint64_t nwaves = (uint64_t)grid * (kThreads / 64);
+    constexpr int kWaves = kDecThreads / 64;
+    const int grid = (int)std::min<uint64_t>((waves_needed + kWaves - 1) / kWaves, (uint64_t)dec_grid_cap(ctx));
+    const uint64_t nwaves = (uint64_t)grid * kWaves;
     uint64_t bpw = (nblocks + nwaves - 1) / nwaves;
     bpw = (bpw + step - 1) / step * step;
     st = alias_iv(ctx, &iv_in, iv_out, npayloads, stream);
@@ -145,8 +146,9 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     a.step_r = (uint32_t)(step % bpp);
     a.iv_in = iv_in;
     a.iv_out = iv_out;
-    a.tables = ctx->d_tables + 512;
+    a.tables = ctx->d_tables + kDecTableOff / 4;
     a.status = ctx->d_status;
+    a.inplace = in == out;
     if (in == out && nwaves > 1) {
         st = ensure(&ctx->d_boundary, &ctx->boundary_cap, nwaves);
         if (st) return st;
@@ -172,9 +174,11 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.npayloads = npayloads;
     a.iv_in = iv_in;
     a.iv_out = iv_out;
-    a.tables = ctx->d_tables + 512;
+    a.tables = ctx->d_tables + kDecTableOff / 4;
     a.status = ctx->d_status;
-    const int grid = (int)std::min<uint64_t>((npayloads + 7) / 8, (uint64_t)wg_cap(ctx));
+    a.inplace = in == out;
+    constexpr int kWaves = kDecThreads / 64;
+    const int grid = (int)std::min<uint64_t>((npayloads + kWaves - 1) / kWaves, (uint64_t)dec_grid_cap(ctx));
     ctx->last_stream = stream;
     return map_err(launch_decrypt_ragged(a, grid, stream));
 }
@@ -228,9 +232,9 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     ctx->num_cus = prop.multiProcessorCount;
     const HostTables& t = host_tables();
     uint8_t host[kTablesBytes];
-    memcpy(host, t.enc, sizeof(t.enc));
-    memcpy(host + 2048, t.dec, sizeof(t.dec));
-    memcpy(host + 4096, t.sbox, 256);
+    memcpy(host + kEncTableOff, t.enc, sizeof(t.enc));
+    memcpy(host + kDecTableOff, t.dec, sizeof(t.dec));
+    memcpy(host + kSboxOff, t.sbox, 256);
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tables), kTablesBytes);
     if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, host, kTablesBytes, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_status), 16);
@@ -296,7 +300,7 @@ int cyaes_gpu_set_keys_device(cyaes_gpu* ctx, const uint8_t* d_keys, uint32_t nk
     DeviceGuard g(ctx->device);
     int st = reserve_keys(ctx, nkeys);
     if (st) return st;
-    const uint8_t* d_sbox = reinterpret_cast<const uint8_t*>(ctx->d_tables) + 4096;
+    const uint8_t* d_sbox = reinterpret_cast<const uint8_t*>(ctx->d_tables) + kSboxOff;
     CY_TRY(launch_key_expand(d_keys, nkeys, d_sbox, ctx->d_keys, (hipStream_t)stream));
     ctx->nkeys = nkeys;
     ctx->last_stream = (hipStream_t)stream;

@@ -47,8 +47,10 @@ HostTables build() {
         const uint32_t tl1 = le(mul(s, 2), s, s, mul(s, 3));
         t.enc[v] = tl1;
         t.enc[256 + v] = rotl(tl1, 16);
-        t.dec[v] = le(mul(si, 14), mul(si, 9), mul(si, 13), mul(si, 11));
-        t.dec[256 + v] = (uint32_t)si * 0x01010101u;
+        const uint32_t tl5 = le(mul(si, 14), mul(si, 9), mul(si, 13), mul(si, 11));
+        t.dec[v] = tl5;
+        t.dec[256 + v] = rotl(tl5, 16);
+        t.dec[512 + v] = (uint32_t)si * 0x01010101u;
     }
     return t;
 }
@@ -104,19 +106,28 @@ void expand_key(const uint8_t key[16], cyaes_key* out) {
         }
 }
 
+// Middle rounds are stored rotr8 so the kernels can fold the key into the
+// rotated half of a column (cyaes_kernels.hip, col()).
+static uint32_t to_dev(uint32_t w, int r) {
+    const uint32_t v = bswap(w);
+    return (r > 0 && r < CYAES_ROUNDS) ? rotl(v, 24) : v;
+}
+
+static uint32_t from_dev(uint32_t v, int r) { return bswap((r > 0 && r < CYAES_ROUNDS) ? rotl(v, 8) : v); }
+
 void to_device_schedule(const cyaes_key& k, uint32_t out[88]) {
     for (int r = 0; r <= CYAES_ROUNDS; r++)
         for (int c = 0; c < 4; c++) {
-            out[4 * r + c] = bswap(k.ke[r][c]);
-            out[44 + 4 * r + c] = bswap(k.kd[r][c]);
+            out[4 * r + c] = to_dev(k.ke[r][c], r);
+            out[44 + 4 * r + c] = to_dev(k.kd[r][c], r);
         }
 }
 
 void from_device_schedule(const uint32_t in[88], cyaes_key* k) {
     for (int r = 0; r <= CYAES_ROUNDS; r++)
         for (int c = 0; c < 4; c++) {
-            k->ke[r][c] = bswap(in[4 * r + c]);
-            k->kd[r][c] = bswap(in[44 + 4 * r + c]);
+            k->ke[r][c] = from_dev(in[4 * r + c], r);
+            k->kd[r][c] = from_dev(in[44 + 4 * r + c], r);
         }
 }
 
