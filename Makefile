@@ -22,7 +22,7 @@ HDRS     := include/cyaes.h include/cyclone_amd/cyr_rijndael.h cyclone_amd/csrc/
 KOBJ     := $(BUILD)/cyaes_kernels.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
-.PHONY: all lib oracle cpptest clean
+.PHONY: all lib oracle cpptest microbench clean
 all: lib oracle cpptest
 lib: $(LIB)
 oracle: $(ORACLE)
@@ -45,6 +45,11 @@ $(ORACLE): oracle/aes_oracle.c
 
 $(CPPTEST): tests/cpp/test_rijndael.cpp $(LIB) $(HDRS)
 	$(CXX) -O2 -std=c++17 -Wall $(INC) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
+
+microbench: $(BUILD)/microbench
+
+$(BUILD)/microbench: tools/microbench.hip | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(ORACLE)

@@ -81,15 +81,25 @@ __device__ __forceinline__ uint32_t fastdiv(uint32_t n, const Fastdiv& f) {
     return (uint32_t)((hi + (lo >> 32)) >> 32);
 }
 
-// One middle-round column.  x0..x3 supply bytes b0..b3; A-table reads for
-// b0/b1, B-table reads for b2/b3; kr = rotr8(round key word).
-__device__ __forceinline__ uint32_t col(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
-                                        uint32_t x3, uint32_t kr) {
+// Decrypt middle-round column.  x0..x3 supply bytes b0..b3; A-table reads
+// for b0/b1, B-table reads for b2/b3; kr = rotr8(round key word).
+__device__ __forceinline__ uint32_t dcol(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
+                                         uint32_t x3, uint32_t kr) {
     const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));
     const uint32_t l1 = ld(lds, addr(x1, lo, kSel1));
     const uint32_t l2 = ld(lds + kHalfB, addr(x2, lo, kSel2));
     const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, kSel3));
     return xor3(l0, l2, rotl8(xor3(l1, l3, kr)));
+}
+
+// Encrypt middle-round column: all four T-tables resident, no rotation.
+__device__ __forceinline__ uint32_t ecol(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
+                                         uint32_t x3, uint32_t k) {
+    const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));                   // TL1[b0]
+    const uint32_t l1 = ld(lds + kHalfB, addr(x1, lo, kSel1));          // TL2[b1]
+    const uint32_t l2 = ld(lds, addr(x2, lo, region1(kSel2)));          // TL3[b2]
+    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, region1(kSel3))); // TL4[b3]
+    return xor3(l0, l1, xor3(l2, l3, k));
 }
 
 // Merge the four last-round bytes (byte j of word j-th lookup).
@@ -98,15 +108,16 @@ __device__ __forceinline__ uint32_t merge4(uint32_t l0, uint32_t l1, uint32_t l2
 }
 
 // ---- encryption (_encryptBlock, cyr_rijndael.cpp:638-705) -----------------
-// Rows: A = TL1 (LE bytes 2s,s,s,3s), B = TL3 = rotl16(TL1); TL2/TL4 = rotl8.
-// Column j takes b0(u_j), b1(u_j+1), b2(u_j+2), b3(u_j+3) (ShiftRows).
-// Last round: S[x] is byte0/byte3 of TL3 and byte1/byte2 of TL1.
+// Region 0 rows: A = TL1 (LE bytes 2s,s,s,3s), B = TL2; region 1: A = TL3,
+// B = TL4 (rotl8/16/24 of TL1).  Column j takes b0(u_j), b1(u_j+1),
+// b2(u_j+2), b3(u_j+3) (ShiftRows).  Last round: S[x] is byte0/byte3 of TL3
+// and byte1/byte2 of TL1.
 __device__ __forceinline__ uint32_t enc_last(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
                                              uint32_t x3) {
-    const uint32_t l0 = ld(lds + kHalfB, addr(x0, lo, kSel0));
+    const uint32_t l0 = ld(lds, addr(x0, lo, region1(kSel0)));
     const uint32_t l1 = ld(lds, addr(x1, lo, kSel1));
     const uint32_t l2 = ld(lds, addr(x2, lo, kSel2));
-    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, kSel3));
+    const uint32_t l3 = ld(lds, addr(x3, lo, region1(kSel3)));
     return merge4(l0, l1, l2, l3);
 }
 
@@ -115,10 +126,10 @@ __device__ __forceinline__ void enc_block(const char* lds, uint32_t lo, const ui
                                           uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
 #pragma unroll
     for (int r = 1; r < 10; r++) {
-        const uint32_t a0 = col(lds, lo, s0, s1, s2, s3, ek[4 * r + 0]);
-        const uint32_t a1 = col(lds, lo, s1, s2, s3, s0, ek[4 * r + 1]);
-        const uint32_t a2 = col(lds, lo, s2, s3, s0, s1, ek[4 * r + 2]);
-        const uint32_t a3 = col(lds, lo, s3, s0, s1, s2, ek[4 * r + 3]);
+        const uint32_t a0 = ecol(lds, lo, s0, s1, s2, s3, ek[4 * r + 0]);
+        const uint32_t a1 = ecol(lds, lo, s1, s2, s3, s0, ek[4 * r + 1]);
+        const uint32_t a2 = ecol(lds, lo, s2, s3, s0, s1, ek[4 * r + 2]);
+        const uint32_t a3 = ecol(lds, lo, s3, s0, s1, s2, ek[4 * r + 3]);
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     }
     const uint32_t o0 = enc_last(lds, lo, s0, s1, s2, s3) ^ ek[40];
@@ -142,22 +153,39 @@ __device__ __forceinline__ uint32_t dec_last(const char* lds, uint32_t lo, uint3
     return merge4(l0, l1, l2, l3);
 }
 
-// Returns D(c) ^ prev (CBC, cyr_rijndael.cpp:625-630).
-__device__ __forceinline__ uint4 dec_cbc(const char* lds, uint32_t lo, const uint32_t* __restrict__ dk, uint4 c,
-                                         uint4 prev) {
-    uint32_t s0 = c.x ^ dk[0], s1 = c.y ^ dk[1], s2 = c.z ^ dk[2], s3 = c.w ^ dk[3];
+// Decrypts N independent blocks together (N-way ILP per LDS round trip) and
+// returns D(c[n]) ^ prev[n] in prev[n] (CBC, cyr_rijndael.cpp:625-630).
+template <int N>
+__device__ __forceinline__ void dec_cbc(const char* lds, uint32_t lo, const uint32_t* __restrict__ dk,
+                                        const uint4 (&c)[N], uint4 (&prev)[N]) {
+    uint32_t s[N][4];
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        s[n][0] = c[n].x ^ dk[0]; s[n][1] = c[n].y ^ dk[1];
+        s[n][2] = c[n].z ^ dk[2]; s[n][3] = c[n].w ^ dk[3];
+    }
 #pragma unroll
     for (int r = 1; r < 10; r++) {
-        const uint32_t a0 = col(lds, lo, s0, s3, s2, s1, dk[4 * r + 0]);
-        const uint32_t a1 = col(lds, lo, s1, s0, s3, s2, dk[4 * r + 1]);
-        const uint32_t a2 = col(lds, lo, s2, s1, s0, s3, dk[4 * r + 2]);
-        const uint32_t a3 = col(lds, lo, s3, s2, s1, s0, dk[4 * r + 3]);
-        s0 = a0; s1 = a1; s2 = a2; s3 = a3;
+        uint32_t t[N][4];
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            t[n][0] = dcol(lds, lo, s[n][0], s[n][3], s[n][2], s[n][1], dk[4 * r + 0]);
+            t[n][1] = dcol(lds, lo, s[n][1], s[n][0], s[n][3], s[n][2], dk[4 * r + 1]);
+            t[n][2] = dcol(lds, lo, s[n][2], s[n][1], s[n][0], s[n][3], dk[4 * r + 2]);
+            t[n][3] = dcol(lds, lo, s[n][3], s[n][2], s[n][1], s[n][0], dk[4 * r + 3]);
+        }
+#pragma unroll
+        for (int n = 0; n < N; n++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) s[n][j] = t[n][j];
     }
-    return make_uint4(xor3(dec_last(lds, lo, s0, s3, s2, s1), dk[40], prev.x),
-                      xor3(dec_last(lds, lo, s1, s0, s3, s2), dk[41], prev.y),
-                      xor3(dec_last(lds, lo, s2, s1, s0, s3), dk[42], prev.z),
-                      xor3(dec_last(lds, lo, s3, s2, s1, s0), dk[43], prev.w));
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        prev[n] = make_uint4(xor3(dec_last(lds, lo, s[n][0], s[n][3], s[n][2], s[n][1]), dk[40], prev[n].x),
+                             xor3(dec_last(lds, lo, s[n][1], s[n][0], s[n][3], s[n][2]), dk[41], prev[n].y),
+                             xor3(dec_last(lds, lo, s[n][2], s[n][1], s[n][0], s[n][3]), dk[42], prev[n].z),
+                             xor3(dec_last(lds, lo, s[n][3], s[n][2], s[n][1], s[n][0]), dk[43], prev[n].w));
+    }
 }
 
 // Key index of payload p (cyaes.h): key_idx[p] | p / ppk | 0, clamped.
@@ -181,13 +209,14 @@ __device__ __forceinline__ void drain_loads() { asm volatile("s_waitcnt vmcnt(0)
 
 // ---- CBC encrypt: one lane per payload chain (cyr_rijndael.cpp:588-609) ----
 template <bool RAGGED, bool KEYED>
-__global__ __launch_bounds__(kEncThreads, 2) void k_encrypt(EncArgs a) {
+__global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
     fill_region(lds_words, a.tables, a.tables + 256, kEncThreads);
+    fill_region(lds_words + 16384, a.tables + 512, a.tables + 768, kEncThreads);
     __syncthreads();
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lo = (threadIdx.x & 31u) << 2;
+    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
     const uint64_t wstride = (uint64_t)gridDim.x * kEncThreads;
     const uint64_t wbase0 = (uint64_t)blockIdx.x * kEncThreads + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
 
@@ -248,11 +277,13 @@ __global__ __launch_bounds__(kEncThreads, 2) void k_encrypt(EncArgs a) {
 // ---- CBC decrypt, uniform contiguous batch: one lane per block ------------
 // The batch is one array of nblocks blocks; payload boundaries every bpp
 // blocks restart the chain at the IV.  Each wave owns the contiguous range
-// [w*bpw, (w+1)*bpw) and walks it in steps of 64*R blocks.  BIG: bpp >= 64*R,
-// so a step crosses at most one payload boundary and no division is needed.
+// [w*bpw, (w+1)*bpw) (bpw a multiple of 64*R) and walks it in steps of 64*R
+// blocks: R rows of 64 lanes, decrypted two rows at a time.  BIG: bpp >= 64*R,
+// so a step holds at most one payload start and needs no division.
 template <bool KEYED, bool BIG>
 __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     constexpr int R = kDecRows;
+    static_assert(R % 2 == 0, "rows are decrypted in pairs");
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
     fill_region(lds_words, a.tables, a.tables + 256, kDecThreads);
     fill_region(lds_words + 16384, a.tables + 512, nullptr, kDecThreads);
@@ -271,56 +302,120 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     const uint4* in = reinterpret_cast<const uint4*>(a.in);
     uint4* out = reinterpret_cast<uint4*>(a.out);
     const bool inplace = a.inplace != 0;
+    const uint32_t back = lane ? 1u : 0u;         // lane 0 takes its chain from `carry`
 
-    uint4 carry = make_uint4(0, 0, 0, 0);         // C[begin-1]
+    uint4 carry = make_uint4(0, 0, 0, 0);         // C[base-1]
     if (bpos != 0) carry = a.boundary ? a.boundary[wave] : in[begin - 1];
     const uint32_t* __restrict__ dk0 = a.keys.table + 44;
 
-    for (uint64_t base = begin; base < end; base += 64 * R) {
-        uint4 c[R], pv[R];
-#pragma unroll
-        for (int k = 0; k < R; k++) {
-            const uint64_t g = base + 64 * k + lane;
-            const bool valid = g < end;
-            c[k] = valid ? in[g] : make_uint4(0, 0, 0, 0);
-            pv[k] = (valid && (k > 0 || lane > 0)) ? in[g - 1] : carry;
+    // Position of row k's block in its payload (r) and the payload index (p).
+    auto position = [&](int k, uint32_t& r, uint64_t& p) {
+        const uint32_t lpos = bpos + 64 * k + lane;
+        if (BIG) {
+            r = min(lpos, lpos - bpp);
+            p = bp + (lpos >= bpp ? 1 : 0);
+        } else {
+            const uint32_t q = fastdiv(lpos, a.bpp);
+            r = lpos - q * bpp;
+            p = bp + q;
         }
-        if (inplace) drain_loads();
+    };
+
+    for (uint64_t base = begin; base < end; base += 64 * R) {
+        const bool full = base + 64 * R <= end;
+        const uint4* src = in + base + lane;
+        uint4 c[R], pv[R];
+        if (full) {
 #pragma unroll
-        for (int k = 0; k < R; k++) {
-            const uint64_t g = base + 64 * k + lane;
-            const bool valid = g < end;
-            const uint32_t lpos = bpos + 64 * k + lane;
-            uint32_t r;
-            uint64_t p;
-            if (BIG) {
-                r = min(lpos, lpos - bpp);
-                p = bp + (lpos >= bpp ? 1 : 0);
-            } else {
-                const uint32_t q = fastdiv(lpos, a.bpp);
-                r = lpos - q * bpp;
-                p = bp + q;
+            for (int k = 0; k < R; k++) c[k] = src[64 * k];
+            pv[0] = *(src - back);
+#pragma unroll
+            for (int k = 1; k < R; k++) pv[k] = src[64 * k - 1];
+        } else {  // last, partial step of the batch: clamp reads into range
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const uint64_t g = min(base + 64 * k + lane, end - 1);
+                c[k] = in[g];
+                pv[k] = in[g - ((k == 0) ? back : 1u)];
             }
-            uint4 prev = pv[k];
-            if (r == 0) prev = (a.iv_in && valid) ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
-            if (!KEYED) {
-                const uint4 d = dec_cbc(lds, lo, dk0, c[k], prev);
-                if (valid) out[g] = d;
-            } else {
+        }
+        if (lane == 0) pv[0] = carry;
+        if (inplace) drain_loads();
+        // Chain restarts at payload starts inside this step.
+        if (BIG) {
+            const uint32_t fo = bpos == 0 ? 0u : bpp - bpos;  // offset of the payload start, if < 64R
+            if (fo < 64u * R) {
+                const uint64_t pf = bp + (bpos == 0 ? 0 : 1);
+                const uint4 ivv = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * pf) : default_iv();
+#pragma unroll
+                for (int k = 0; k < R; k++)
+                    if ((fo >> 6) == (uint32_t)k && lane == (fo & 63u)) pv[k] = ivv;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                uint32_t r;
+                uint64_t p;
+                position(k, r, p);
+                if (r == 0) {
+                    const bool valid = base + 64 * k + lane < end;
+                    pv[k] = (a.iv_in && valid) ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
+                }
+            }
+        }
+        if (a.iv_out) {  // final chain block of each payload ending in this step
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                uint32_t r;
+                uint64_t p;
+                position(k, r, p);
+                if (r == bpp - 1 && base + 64 * k + lane < end) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+            }
+        }
+        uint4 d[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) d[k] = pv[k];
+        if (!KEYED) {
+#pragma unroll
+            for (int k = 0; k < R; k += 2) {  // two rows per LDS round trip (4-way measured slower)
+                const uint4 cc[2] = {c[k], c[k + 1]};
+                uint4 dd[2] = {d[k], d[k + 1]};
+                dec_cbc<2>(lds, lo, dk0, cc, dd);
+                d[k] = dd[0];
+                d[k + 1] = dd[1];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                uint32_t r;
+                uint64_t p;
+                position(k, r, p);
+                const bool valid = base + 64 * k + lane < end;
                 const uint32_t kid = key_index(a.keys, p, valid, a.status);
                 bool pending = valid;
-                while (true) {
+                while (true) {  // waterfall over the distinct keys of this row
                     const uint64_t m = __ballot(pending);
                     if (m == 0) break;
                     const uint32_t ku = __builtin_amdgcn_readlane(kid, __builtin_ctzll(m));
                     if (pending && kid == ku) {
                         pending = false;
                         const uint32_t* __restrict__ dk = a.keys.table + (uint64_t)ku * kSchedWords + 44;
-                        out[g] = dec_cbc(lds, lo, dk, c[k], prev);
+                        const uint4 cc[1] = {c[k]};
+                        uint4 dd[1] = {d[k]};
+                        dec_cbc<1>(lds, lo, dk, cc, dd);
+                        d[k] = dd[0];
                     }
                 }
             }
-            if (a.iv_out && valid && r == bpp - 1) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+        }
+        uint4* dst = out + base + lane;
+        if (full) {
+#pragma unroll
+            for (int k = 0; k < R; k++) dst[64 * k] = d[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < R; k++)
+                if (base + 64 * k + lane < end) dst[64 * k] = d[k];
         }
         carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
         bpos += a.step_r;
@@ -370,9 +465,18 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 const uint32_t g = base + 64 * k + lane;
-                const uint4 d = dec_cbc(lds, lo, dk, c[k], pv[k]);
-                if (g < nb) out[g] = d;
                 if (a.iv_out && g + 1 == nb) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+            }
+#pragma unroll
+            for (int k = 0; k < R; k += 2) {
+                const uint4 cc[2] = {c[k], c[k + 1]};
+                uint4 dd[2] = {pv[k], pv[k + 1]};
+                dec_cbc<2>(lds, lo, dk, cc, dd);
+#pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    const uint32_t g = base + 64 * (k + n) + lane;
+                    if (g < nb) out[g] = dd[n];
+                }
             }
             carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
         }
@@ -419,12 +523,9 @@ __global__ void k_key_expand(const uint8_t* keys, uint32_t nkeys, const uint8_t*
         }
         w[j] = w[j - 4] ^ t;
     }
-    // Device layout (cyaes_internal.h): LE words, rounds 1..9 rotated right by 8.
+    // Device layout (cyaes_internal.h): LE words, dk rounds 1..9 rotated right by 8.
     uint32_t* s = sched + (uint64_t)i * kSchedWords;
-    for (int j = 0; j < 44; j++) {
-        const uint32_t v = __builtin_bswap32(w[j]);
-        s[j] = (j >= 4 && j < 40) ? __builtin_rotateright32(v, 8) : v;
-    }
+    for (int j = 0; j < 44; j++) s[j] = __builtin_bswap32(w[j]);
     for (int r = 0; r <= 10; r++) {
         for (int c = 0; c < 4; c++) {
             uint32_t t = w[4 * (10 - r) + c];

@@ -46,7 +46,9 @@ HostTables build() {
         const uint8_t s = t.sbox[v], si = t.inv_sbox[v];
         const uint32_t tl1 = le(mul(s, 2), s, s, mul(s, 3));
         t.enc[v] = tl1;
-        t.enc[256 + v] = rotl(tl1, 16);
+        t.enc[256 + v] = rotl(tl1, 8);
+        t.enc[512 + v] = rotl(tl1, 16);
+        t.enc[768 + v] = rotl(tl1, 24);
         const uint32_t tl5 = le(mul(si, 14), mul(si, 9), mul(si, 13), mul(si, 11));
         t.dec[v] = tl5;
         t.dec[256 + v] = rotl(tl5, 16);
@@ -106,28 +108,25 @@ void expand_key(const uint8_t key[16], cyaes_key* out) {
         }
 }
 
-// Middle rounds are stored rotr8 so the kernels can fold the key into the
-// rotated half of a column (cyaes_kernels.hip, col()).
-static uint32_t to_dev(uint32_t w, int r) {
-    const uint32_t v = bswap(w);
-    return (r > 0 && r < CYAES_ROUNDS) ? rotl(v, 24) : v;
-}
-
-static uint32_t from_dev(uint32_t v, int r) { return bswap((r > 0 && r < CYAES_ROUNDS) ? rotl(v, 8) : v); }
+// Decryption middle rounds are stored rotr8 so the decrypt kernels can fold
+// the key into the rotated half of a column (cyaes_kernels.hip, dcol()).
+static bool rotated(int r) { return r > 0 && r < CYAES_ROUNDS; }
 
 void to_device_schedule(const cyaes_key& k, uint32_t out[88]) {
     for (int r = 0; r <= CYAES_ROUNDS; r++)
         for (int c = 0; c < 4; c++) {
-            out[4 * r + c] = to_dev(k.ke[r][c], r);
-            out[44 + 4 * r + c] = to_dev(k.kd[r][c], r);
+            out[4 * r + c] = bswap(k.ke[r][c]);
+            const uint32_t d = bswap(k.kd[r][c]);
+            out[44 + 4 * r + c] = rotated(r) ? rotl(d, 24) : d;
         }
 }
 
 void from_device_schedule(const uint32_t in[88], cyaes_key* k) {
     for (int r = 0; r <= CYAES_ROUNDS; r++)
         for (int c = 0; c < 4; c++) {
-            k->ke[r][c] = from_dev(in[4 * r + c], r);
-            k->kd[r][c] = from_dev(in[44 + 4 * r + c], r);
+            k->ke[r][c] = bswap(in[4 * r + c]);
+            const uint32_t d = in[44 + 4 * r + c];
+            k->kd[r][c] = bswap(rotated(r) ? rotl(d, 8) : d);
         }
 }
 
