@@ -129,24 +129,21 @@ def main():
     if args.payloads:
         npay = args.payloads
     nbytes = npay * pb
-    p0 = rank * npay
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
 
+    from cyclone_amd import dist as cdist
+
     ctx = ca.GpuContext(local)
-    # Session key(s): rank 0 owns them (DH secret in the relay), RCCL-broadcast to all GPUs.
-    nkeys = (npay * world + ppk - 1) // ppk if ppk else 1
-    if rank == 0:
-        raw = session_keys(nkeys) if ppk else bytes(range(16))
-        d_keys = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda")
-    else:
-        d_keys = torch.zeros(16 * nkeys, dtype=torch.uint8, device="cuda")
-    if world > 1:
-        dist.broadcast(d_keys, src=0)
-    if ppk:  # this rank's sessions only
-        first = p0 // ppk
-        d_keys = d_keys[16 * first: 16 * (first + (npay + ppk - 1) // ppk)].contiguous()
-    ctx.set_keys_device(d_keys, d_keys.numel() // 16, sh)
+    # Session key(s): rank 0 owns them (the relay's DH secret), RCCL-broadcast
+    # over xGMI straight into device memory; each GPU expands its own sessions.
+    p0, npay = cdist.weak_shard(npay, rank)
+    nkeys = cdist.session_range(0, npay * world, ppk)[1]
+    d_keys = cdist.broadcast_keys((session_keys(nkeys) if ppk else bytes(range(16))) if rank == 0 else None,
+                                  nkeys, "cuda")
+    k0, nk = cdist.session_range(p0, npay, ppk)
+    d_keys = d_keys[16 * k0: 16 * (k0 + nk)].contiguous()
+    ctx.set_keys_device(d_keys, nk, sh)
 
     log("rank %d/%d: config %s, %d payloads x %d B = %.2f GiB per GPU, %d CUs"
         % (rank, world, args.config, npay, pb, nbytes / 2**30, ctx.num_cus))
@@ -176,7 +173,7 @@ def main():
         dr = ctx.digest(d_rt, nbytes, sh)
         ok = dr == dp
         g = golden.get(gname) if gname else None
-        if g and g["npayloads"] == npay and g["payload_bytes"] == pb:
+        if g and g["npayloads"] == npay and g["payload_bytes"] == pb and g["p0"] == p0:
             ok = ok and ["%016x" % v for v in dc] == g["cipher_digest"] and ["%016x" % v for v in dp] == g["plain_digest"]
         ok = ok and ctx.check() == ca.CYAES_OK
         flag = torch.tensor([0 if ok else 1], device="cuda")

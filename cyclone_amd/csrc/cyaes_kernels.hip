@@ -12,21 +12,23 @@
 //  * T-tables live in LDS as 256 rows x 256 B: row x holds A[x] replicated in
 //    32 slots and B[x] in the next 32.  A lookup address is one v_perm_b32,
 //    (x << 8) | (lane&31)*4, and lane l always hits bank l%32: the gathers are
-//    bank-conflict-free.  Each direction keeps two of its four T-tables
-//    (encrypt TL1/TL3, decrypt TL5/TL7); the other two are rotl8 of those, and
-//    a column needs a single rotation because rotation distributes over XOR:
-//        col = TA[b0] ^ TB[b2] ^ rotl8(TA[b1] ^ TB[b3] ^ rotr8(k)).
-//    The round keys of rounds 1..9 are stored pre-rotated (rotr8(k)), so a
-//    column is xor3, rotate, xor3 (v_bitop3_b32).  The last round's S-box
-//    bytes come from TL1/TL3 bytes (encrypt) or a Si x 0x01010101 region
-//    (decrypt), merged with v_bfi_b32.
+//    bank-conflict-free.  A second 64 KiB region is selected through byte 2 of
+//    the lane-offset register, still one v_perm_b32.
+//    Encrypt keeps all four T-tables (TL1|TL2, TL3|TL4): a column is
+//        xor3(TL1[b0], TL2[b1], xor3(TL3[b2], TL4[b3], k)).
+//    Decrypt keeps TL5|TL7 and Si; TL6/TL8 are rotl8 of those and a column
+//    needs one rotation because rotation distributes over XOR:
+//        col = TL5[b0] ^ TL7[b2] ^ rotl8(TL5[b1] ^ TL7[b3] ^ rotr8(k)),
+//    with the decryption round keys of rounds 1..9 stored pre-rotated.
+//    The last round's S-box bytes come from TL1/TL3 bytes (encrypt) or the
+//    Si x 0x01010101 region (decrypt), merged with v_bfi_b32 / v_perm_b32.
 //  * Round keys are wave-uniform and live in SGPRs (s_load from the key table;
 //    a per-payload key index is handled by a waterfall over the distinct keys
 //    present in a wave, normally one).
 //  * Encrypt (serial CBC): one lane = one payload chain, 8 blocks (128 B, one
 //    full line per lane) loaded per step.
-//  * Decrypt (block-parallel): one lane = one 16-B block, each wave-instruction
-//    loads 1 KiB contiguous; the previous ciphertext block is a second load at
+//  * Decrypt (block-parallel): one lane = one 16-B block, two rows decrypted
+//    together, each wave-instruction loads 1 KiB contiguous; the previous ciphertext block is a second load at
 //    offset -16 (an L1/L2 hit), the wave's chain across steps is carried in
 //    registers.
 #include "cyaes_internal.h"
