@@ -282,6 +282,137 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
 // [w*bpw, (w+1)*bpw) (bpw a multiple of 64*R) and walks it in steps of 64*R
 // blocks: R rows of 64 lanes, decrypted two rows at a time.  BIG: bpp >= 64*R,
 // so a step holds at most one payload start and needs no division.
+// Per-wave walk state of k_decrypt_flat (kept in registers: passed by value
+// and returned, never through memory).
+struct FlatPos {
+    uint64_t bp;    // payload of the step's first block
+    uint32_t bpos;  // its position in the payload
+};
+
+// Position of row k's block in its payload (r) and the payload index (p).
+template <bool BIG>
+__device__ __forceinline__ void flat_position(const DecArgs& a, FlatPos ps, uint32_t lane, int k, uint32_t& r,
+                                              uint64_t& p) {
+    const uint32_t lpos = ps.bpos + 64 * k + lane;
+    const uint32_t bpp = a.bpp.d;
+    if (BIG) {
+        r = min(lpos, lpos - bpp);
+        p = ps.bp + (lpos >= bpp ? 1 : 0);
+    } else {
+        const uint32_t q = fastdiv(lpos, a.bpp);
+        r = lpos - q * bpp;
+        p = ps.bp + q;
+    }
+}
+
+// One step of R rows at block `base`.  FULL: all 64*R blocks are in range
+// (every step but possibly the batch's last), so loads and stores are
+// unguarded and use immediate offsets off one lane pointer.
+template <bool KEYED, bool BIG, bool FULL>
+__device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, uint32_t lo, uint32_t lane,
+                                           uint64_t base, uint64_t end, FlatPos ps, uint4 carry) {
+    constexpr int R = kDecRows;
+    const uint4* __restrict__ in = reinterpret_cast<const uint4*>(a.in);
+    uint4* out = reinterpret_cast<uint4*>(a.out);
+    const uint64_t back = lane ? 1u : 0u;  // lane 0 reads its own block (replaced by carry)
+    uint4 c[R], pv[R];
+    if (FULL) {
+        const uint64_t g0 = base + lane;
+#pragma unroll
+        for (int k = 0; k < R; k++) c[k] = in[g0 + 64 * k];
+        pv[0] = in[g0 - back];
+#pragma unroll
+        for (int k = 1; k < R; k++) pv[k] = in[g0 + 64 * k - 1];
+    } else {  // last, partial step of the batch: clamp reads into range
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const uint64_t g = min(base + 64 * k + lane, end - 1);
+            c[k] = in[g];
+            pv[k] = in[g - ((k == 0) ? back : 1u)];
+        }
+    }
+    if (lane == 0) pv[0] = carry;
+    if (a.inplace) drain_loads();
+    // Chain restarts at payload starts inside this step.
+    if (BIG) {
+        const uint32_t fo = ps.bpos == 0 ? 0u : a.bpp.d - ps.bpos;  // offset of the payload start, if < 64R
+        if (fo < 64u * R) {
+            const uint64_t pf = ps.bp + (ps.bpos == 0 ? 0 : 1);
+            const uint4 ivv = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * pf) : default_iv();
+#pragma unroll
+            for (int k = 0; k < R; k++)
+                if ((fo >> 6) == (uint32_t)k && lane == (fo & 63u)) pv[k] = ivv;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            uint32_t r;
+            uint64_t p;
+            flat_position<BIG>(a, ps, lane, k, r, p);
+            if (r == 0) {
+                const bool valid = FULL || base + 64 * k + lane < end;
+                pv[k] = (a.iv_in && valid) ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
+            }
+        }
+    }
+    if (a.iv_out) {  // final chain block of each payload ending in this step
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            uint32_t r;
+            uint64_t p;
+            flat_position<BIG>(a, ps, lane, k, r, p);
+            if (r == a.bpp.d - 1 && (FULL || base + 64 * k + lane < end))
+                *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+        }
+    }
+    uint4 d[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) d[k] = pv[k];
+    if (!KEYED) {
+        const uint32_t* __restrict__ dk0 = a.keys.table + 44;
+#pragma unroll
+        for (int k = 0; k < R; k += 2) {  // two rows per LDS round trip (4-way measured slower)
+            const uint4 cc[2] = {c[k], c[k + 1]};
+            uint4 dd[2] = {d[k], d[k + 1]};
+            dec_cbc<2>(lds, lo, dk0, cc, dd);
+            d[k] = dd[0];
+            d[k + 1] = dd[1];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            uint32_t r;
+            uint64_t p;
+            flat_position<BIG>(a, ps, lane, k, r, p);
+            const bool valid = FULL || base + 64 * k + lane < end;
+            const uint32_t kid = key_index(a.keys, p, valid, a.status);
+            bool pending = valid;
+            while (true) {  // waterfall over the distinct keys of this row
+                const uint64_t m = __ballot(pending);
+                if (m == 0) break;
+                const uint32_t ku = __builtin_amdgcn_readlane(kid, __builtin_ctzll(m));
+                if (pending && kid == ku) {
+                    pending = false;
+                    const uint32_t* __restrict__ dk = a.keys.table + (uint64_t)ku * kSchedWords + 44;
+                    const uint4 cc[1] = {c[k]};
+                    uint4 dd[1] = {d[k]};
+                    dec_cbc<1>(lds, lo, dk, cc, dd);
+                    d[k] = dd[0];
+                }
+            }
+        }
+    }
+    if (FULL) {
+#pragma unroll
+        for (int k = 0; k < R; k++) out[base + lane + 64 * k] = d[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < R; k++)
+            if (base + 64 * k + lane < end) out[base + 64 * k + lane] = d[k];
+    }
+    return make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));  // next carry
+}
+
 template <bool KEYED, bool BIG>
 __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     constexpr int R = kDecRows;
@@ -290,140 +421,27 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     fill_region(lds_words, a.tables, a.tables + 256, kDecThreads);
     fill_region(lds_words + 16384, a.tables + 512, nullptr, kDecThreads);
     __syncthreads();
-    const char* lds = reinterpret_cast<const char*>(lds_words);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
     const uint64_t wave =
         (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t begin = wave * a.blocks_per_wave;
     if (begin >= a.nblocks) return;
+    const char* lds = reinterpret_cast<const char*>(lds_words);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
     const uint64_t end = min(begin + a.blocks_per_wave, a.nblocks);
-    const uint32_t bpp = a.bpp.d;
-    uint64_t bp = begin / bpp;                    // payload of the step's first block
-    uint32_t bpos = (uint32_t)(begin - bp * bpp); // its position in the payload
-    const uint4* in = reinterpret_cast<const uint4*>(a.in);
-    uint4* out = reinterpret_cast<uint4*>(a.out);
-    const bool inplace = a.inplace != 0;
-    const uint32_t back = lane ? 1u : 0u;         // lane 0 takes its chain from `carry`
-
-    uint4 carry = make_uint4(0, 0, 0, 0);         // C[base-1]
-    if (bpos != 0) carry = a.boundary ? a.boundary[wave] : in[begin - 1];
-    const uint32_t* __restrict__ dk0 = a.keys.table + 44;
-
-    // Position of row k's block in its payload (r) and the payload index (p).
-    auto position = [&](int k, uint32_t& r, uint64_t& p) {
-        const uint32_t lpos = bpos + 64 * k + lane;
-        if (BIG) {
-            r = min(lpos, lpos - bpp);
-            p = bp + (lpos >= bpp ? 1 : 0);
-        } else {
-            const uint32_t q = fastdiv(lpos, a.bpp);
-            r = lpos - q * bpp;
-            p = bp + q;
-        }
-    };
-
-    for (uint64_t base = begin; base < end; base += 64 * R) {
-        const bool full = base + 64 * R <= end;
-        const uint4* src = in + base + lane;
-        uint4 c[R], pv[R];
-        if (full) {
-#pragma unroll
-            for (int k = 0; k < R; k++) c[k] = src[64 * k];
-            pv[0] = *(src - back);
-#pragma unroll
-            for (int k = 1; k < R; k++) pv[k] = src[64 * k - 1];
-        } else {  // last, partial step of the batch: clamp reads into range
-#pragma unroll
-            for (int k = 0; k < R; k++) {
-                const uint64_t g = min(base + 64 * k + lane, end - 1);
-                c[k] = in[g];
-                pv[k] = in[g - ((k == 0) ? back : 1u)];
-            }
-        }
-        if (lane == 0) pv[0] = carry;
-        if (inplace) drain_loads();
-        // Chain restarts at payload starts inside this step.
-        if (BIG) {
-            const uint32_t fo = bpos == 0 ? 0u : bpp - bpos;  // offset of the payload start, if < 64R
-            if (fo < 64u * R) {
-                const uint64_t pf = bp + (bpos == 0 ? 0 : 1);
-                const uint4 ivv = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * pf) : default_iv();
-#pragma unroll
-                for (int k = 0; k < R; k++)
-                    if ((fo >> 6) == (uint32_t)k && lane == (fo & 63u)) pv[k] = ivv;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < R; k++) {
-                uint32_t r;
-                uint64_t p;
-                position(k, r, p);
-                if (r == 0) {
-                    const bool valid = base + 64 * k + lane < end;
-                    pv[k] = (a.iv_in && valid) ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
-                }
-            }
-        }
-        if (a.iv_out) {  // final chain block of each payload ending in this step
-#pragma unroll
-            for (int k = 0; k < R; k++) {
-                uint32_t r;
-                uint64_t p;
-                position(k, r, p);
-                if (r == bpp - 1 && base + 64 * k + lane < end) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
-            }
-        }
-        uint4 d[R];
-#pragma unroll
-        for (int k = 0; k < R; k++) d[k] = pv[k];
-        if (!KEYED) {
-#pragma unroll
-            for (int k = 0; k < R; k += 2) {  // two rows per LDS round trip (4-way measured slower)
-                const uint4 cc[2] = {c[k], c[k + 1]};
-                uint4 dd[2] = {d[k], d[k + 1]};
-                dec_cbc<2>(lds, lo, dk0, cc, dd);
-                d[k] = dd[0];
-                d[k + 1] = dd[1];
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < R; k++) {
-                uint32_t r;
-                uint64_t p;
-                position(k, r, p);
-                const bool valid = base + 64 * k + lane < end;
-                const uint32_t kid = key_index(a.keys, p, valid, a.status);
-                bool pending = valid;
-                while (true) {  // waterfall over the distinct keys of this row
-                    const uint64_t m = __ballot(pending);
-                    if (m == 0) break;
-                    const uint32_t ku = __builtin_amdgcn_readlane(kid, __builtin_ctzll(m));
-                    if (pending && kid == ku) {
-                        pending = false;
-                        const uint32_t* __restrict__ dk = a.keys.table + (uint64_t)ku * kSchedWords + 44;
-                        const uint4 cc[1] = {c[k]};
-                        uint4 dd[1] = {d[k]};
-                        dec_cbc<1>(lds, lo, dk, cc, dd);
-                        d[k] = dd[0];
-                    }
-                }
-            }
-        }
-        uint4* dst = out + base + lane;
-        if (full) {
-#pragma unroll
-            for (int k = 0; k < R; k++) dst[64 * k] = d[k];
-        } else {
-#pragma unroll
-            for (int k = 0; k < R; k++)
-                if (base + 64 * k + lane < end) dst[64 * k] = d[k];
-        }
-        carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
-        bpos += a.step_r;
-        bp += a.step_q;
-        if (bpos >= bpp) { bpos -= bpp; bp++; }
+    FlatPos ps;
+    ps.bp = begin / a.bpp.d;
+    ps.bpos = (uint32_t)(begin - ps.bp * a.bpp.d);
+    uint4 carry = make_uint4(0, 0, 0, 0);  // C[base-1]
+    if (ps.bpos != 0) carry = a.boundary ? a.boundary[wave] : reinterpret_cast<const uint4*>(a.in)[begin - 1];
+    uint64_t base = begin;
+    for (; base + 64 * R <= end; base += 64 * R) {
+        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry);
+        ps.bpos += a.step_r;
+        ps.bp += a.step_q;
+        if (ps.bpos >= a.bpp.d) { ps.bpos -= a.bpp.d; ps.bp++; }
     }
+    if (base < end) flat_step<KEYED, BIG, false>(a, lds, lo, lane, base, end, ps, carry);
 }
 
 // ---- CBC decrypt, ragged batch: one wave per payload ----------------------
