@@ -22,7 +22,7 @@ HDRS     := include/cyaes.h include/cyclone_amd/cyr_rijndael.h cyclone_amd/csrc/
 KOBJ     := $(BUILD)/cyaes_kernels.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
-.PHONY: all lib oracle cpptest microbench clean
+.PHONY: all lib oracle cpptest microbench variant clean
 all: lib oracle cpptest
 lib: $(LIB)
 oracle: $(ORACLE)
@@ -50,6 +50,12 @@ microbench: $(BUILD)/microbench
 
 $(BUILD)/microbench: tools/microbench.hip | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
+
+# A/B variants: make variant NAME=x DEFS="-DFOO=1" -> build/variants/x.so
+variant: $(HOBJ) | $(BUILD)
+	mkdir -p $(BUILD)/variants
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(KSRC) -o $(BUILD)/variants/$(NAME).o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/$(NAME).so $(BUILD)/variants/$(NAME).o $(HOBJ)
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(ORACLE)

@@ -119,9 +119,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
-    torch.cuda.set_device(local)
+    # Rehearsal knobs for a 1-GPU box (never used by the driver): run every rank
+    # on device 0 and use gloo instead of RCCL.
+    device = 0 if os.environ.get("CYAES_BENCH_SAME_DEVICE") else local
+    backend = os.environ.get("CYAES_DIST_BACKEND", "nccl")
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     import cyclone_amd as ca
 
@@ -134,7 +141,7 @@ def main():
 
     from cyclone_amd import dist as cdist
 
-    ctx = ca.GpuContext(local)
+    ctx = ca.GpuContext(device)
     # Session key(s): rank 0 owns them (the relay's DH secret), RCCL-broadcast
     # over xGMI straight into device memory; each GPU expands its own sessions.
     p0, npay = cdist.weak_shard(npay, rank)

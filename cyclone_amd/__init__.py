@@ -212,8 +212,8 @@ class GpuContext:
     Buffer arguments are device pointers (ints) or torch tensors on the
     context's device; `stream` is a hipStream_t handle (int) or None."""
 
-    def __init__(self, device=0):
-        self._lib = load_library()
+    def __init__(self, device=0, lib=None):
+        self._lib = lib if lib is not None else load_library()
         h = _vp()
         _check(self._lib.cyaes_gpu_create(device, ctypes.byref(h)), "cyaes_gpu_create(%d)" % device)
         self._h = h

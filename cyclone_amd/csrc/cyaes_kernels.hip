@@ -123,6 +123,36 @@ __device__ __forceinline__ uint32_t enc_last(const char* lds, uint32_t lo, uint3
     return merge4(l0, l1, l2, l3);
 }
 
+// N independent states (N-way ILP): s = plaintext ^ chain ^ ek[0..3] on
+// entry, ciphertext on exit.
+template <int N>
+__device__ __forceinline__ void enc_blocks(const char* lds, uint32_t lo, const uint32_t* __restrict__ ek,
+                                           uint32_t (&s)[N][4]) {
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        uint32_t t[N][4];
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            t[n][0] = ecol(lds, lo, s[n][0], s[n][1], s[n][2], s[n][3], ek[4 * r + 0]);
+            t[n][1] = ecol(lds, lo, s[n][1], s[n][2], s[n][3], s[n][0], ek[4 * r + 1]);
+            t[n][2] = ecol(lds, lo, s[n][2], s[n][3], s[n][0], s[n][1], ek[4 * r + 2]);
+            t[n][3] = ecol(lds, lo, s[n][3], s[n][0], s[n][1], s[n][2], ek[4 * r + 3]);
+        }
+#pragma unroll
+        for (int n = 0; n < N; n++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) s[n][j] = t[n][j];
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        const uint32_t o0 = enc_last(lds, lo, s[n][0], s[n][1], s[n][2], s[n][3]) ^ ek[40];
+        const uint32_t o1 = enc_last(lds, lo, s[n][1], s[n][2], s[n][3], s[n][0]) ^ ek[41];
+        const uint32_t o2 = enc_last(lds, lo, s[n][2], s[n][3], s[n][0], s[n][1]) ^ ek[42];
+        const uint32_t o3 = enc_last(lds, lo, s[n][3], s[n][0], s[n][1], s[n][2]) ^ ek[43];
+        s[n][0] = o0; s[n][1] = o1; s[n][2] = o2; s[n][3] = o3;
+    }
+}
+
 // s = plaintext ^ chain ^ ek[0..3] on entry, ciphertext on exit.
 __device__ __forceinline__ void enc_block(const char* lds, uint32_t lo, const uint32_t* __restrict__ ek,
                                           uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
@@ -203,6 +233,26 @@ __device__ __forceinline__ uint32_t key_index(const KeySel& ks, uint64_t p, bool
 
 __device__ __forceinline__ uint32_t rl63(uint32_t v) { return __builtin_amdgcn_readlane(v, 63); }
 
+// Loads one 44-word half of a key schedule (wave-uniform address) into SGPRs.
+// The table is only read by the kernels, but the compiler cannot prove the
+// batch's stores do not alias it, so it would otherwise keep the words in
+// VGPRs or re-load them with vector loads inside the block loop.
+__device__ __forceinline__ void load_sched(const uint32_t* p, uint32_t (&k)[44]) {
+    const uint4* p4 = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 11; i++) {
+        const uint4 v = p4[i];
+#if CYAES_KEYS_VGPR
+        k[4 * i + 0] = v.x; k[4 * i + 1] = v.y; k[4 * i + 2] = v.z; k[4 * i + 3] = v.w;
+#else
+        k[4 * i + 0] = __builtin_amdgcn_readfirstlane(v.x);
+        k[4 * i + 1] = __builtin_amdgcn_readfirstlane(v.y);
+        k[4 * i + 2] = __builtin_amdgcn_readfirstlane(v.z);
+        k[4 * i + 3] = __builtin_amdgcn_readfirstlane(v.w);
+#endif
+    }
+}
+
 __device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kIv2, kIv3); }
 
 // In-place batches: every load of a step must have returned before the step's
@@ -242,7 +292,8 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
             const uint32_t ku = KEYED ? __builtin_amdgcn_readlane(kid, __builtin_ctzll(m)) : 0u;
             if (pending && (!KEYED || kid == ku)) {
                 pending = false;
-                const uint32_t* __restrict__ ek = a.keys.table + (uint64_t)ku * kSchedWords;
+                uint32_t ek[44];
+                load_sched(a.keys.table + (uint64_t)ku * kSchedWords, ek);
                 uint4 c = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
                 const uint4* src = reinterpret_cast<const uint4*>(a.in + off);
                 uint4* dst = reinterpret_cast<uint4*>(a.out + off);
@@ -276,11 +327,95 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     }
 }
 
+#if CYAES_ENC2  // A/B variant (tools/ab.py): measured ~1% slower than k_encrypt on config C
+// ---- CBC encrypt, uniform single-key batch: two chains per lane ----------
+// Lane l of a wave owns payloads wbase+l and wbase+64+l and advances both
+// chains together (2-way ILP per LDS round trip).  Same semantics as k_encrypt.
+constexpr int kEnc2Threads = 512;
+__global__ __launch_bounds__(kEnc2Threads, 1) void k_encrypt2(EncArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
+    fill_region(lds_words, a.tables, a.tables + 256, kEnc2Threads);
+    fill_region(lds_words + 16384, a.tables + 512, a.tables + 768, kEnc2Threads);
+    __syncthreads();
+    const char* lds = reinterpret_cast<const char*>(lds_words);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
+    const uint64_t wstride = (uint64_t)gridDim.x * kEnc2Threads * 2;
+    const uint64_t wbase0 =
+        (uint64_t)blockIdx.x * kEnc2Threads * 2 + 2 * __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+    uint32_t ek[44];
+    load_sched(a.keys.table, ek);
+    const uint32_t nb = a.payload_bytes >> 4;
+    for (uint64_t wbase = wbase0; wbase < a.npayloads; wbase += wstride) {
+        uint64_t p[2] = {wbase + lane, wbase + 64 + lane};
+        const bool act[2] = {p[0] < a.npayloads, p[1] < a.npayloads};
+        if (!act[1]) p[1] = act[0] ? p[0] : 0;  // duplicate work, never stored
+        if (!act[0]) p[0] = 0;
+        uint4 c[2];
+#pragma unroll
+        for (int n = 0; n < 2; n++) c[n] = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p[n]) : default_iv();
+        const uint4* src[2] = {reinterpret_cast<const uint4*>(a.in + p[0] * a.payload_bytes),
+                               reinterpret_cast<const uint4*>(a.in + p[1] * a.payload_bytes)};
+        uint4* dst[2] = {reinterpret_cast<uint4*>(a.out + p[0] * a.payload_bytes),
+                         reinterpret_cast<uint4*>(a.out + p[1] * a.payload_bytes)};
+        uint32_t i = 0;
+        for (; i + 4 <= nb; i += 4) {
+            uint4 b[2][4];
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) b[n][j] = src[n][i + j];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uint32_t st[2][4];
+#pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    st[n][0] = xor3(c[n].x, b[n][j].x, ek[0]); st[n][1] = xor3(c[n].y, b[n][j].y, ek[1]);
+                    st[n][2] = xor3(c[n].z, b[n][j].z, ek[2]); st[n][3] = xor3(c[n].w, b[n][j].w, ek[3]);
+                }
+                enc_blocks<2>(lds, lo, ek, st);
+#pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    c[n] = make_uint4(st[n][0], st[n][1], st[n][2], st[n][3]);
+                    b[n][j] = c[n];
+                }
+            }
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+                if (act[n]) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) dst[n][i + j] = b[n][j];
+                }
+        }
+        for (; i < nb; i++) {
+            uint32_t st[2][4];
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                const uint4 v = src[n][i];
+                st[n][0] = xor3(c[n].x, v.x, ek[0]); st[n][1] = xor3(c[n].y, v.y, ek[1]);
+                st[n][2] = xor3(c[n].z, v.z, ek[2]); st[n][3] = xor3(c[n].w, v.w, ek[3]);
+            }
+            enc_blocks<2>(lds, lo, ek, st);
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                c[n] = make_uint4(st[n][0], st[n][1], st[n][2], st[n][3]);
+                if (act[n]) dst[n][i] = c[n];
+            }
+        }
+        if (a.iv_out) {
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+                if (act[n]) *reinterpret_cast<uint4*>(a.iv_out + 16 * p[n]) = c[n];
+        }
+    }
+}
+#endif  // CYAES_ENC2
+
 // ---- CBC decrypt, uniform contiguous batch: one lane per block ------------
 // The batch is one array of nblocks blocks; payload boundaries every bpp
 // blocks restart the chain at the IV.  Each wave owns the contiguous range
 // [w*bpw, (w+1)*bpw) (bpw a multiple of 64*R) and walks it in steps of 64*R
-// blocks: R rows of 64 lanes, decrypted two rows at a time.  BIG: bpp >= 64*R,
+// blocks: R rows of 64 lanes, decrypted together (R-way ILP).  BIG: bpp >= 64*R,
 // so a step holds at most one payload start and needs no division.
 // Per-wave walk state of k_decrypt_flat (kept in registers: passed by value
 // and returned, never through memory).
@@ -310,7 +445,8 @@ __device__ __forceinline__ void flat_position(const DecArgs& a, FlatPos ps, uint
 // unguarded and use immediate offsets off one lane pointer.
 template <bool KEYED, bool BIG, bool FULL>
 __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, uint32_t lo, uint32_t lane,
-                                           uint64_t base, uint64_t end, FlatPos ps, uint4 carry) {
+                                           uint64_t base, uint64_t end, FlatPos ps, uint4 carry,
+                                           const uint32_t (&dk0)[44]) {
     constexpr int R = kDecRows;
     const uint4* __restrict__ in = reinterpret_cast<const uint4*>(a.in);
     uint4* out = reinterpret_cast<uint4*>(a.out);
@@ -369,15 +505,18 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
 #pragma unroll
     for (int k = 0; k < R; k++) d[k] = pv[k];
     if (!KEYED) {
-        const uint32_t* __restrict__ dk0 = a.keys.table + 44;
+#if CYAES_DEC_ILP2
 #pragma unroll
-        for (int k = 0; k < R; k += 2) {  // two rows per LDS round trip (4-way measured slower)
+        for (int k = 0; k < R; k += 2) {  // two rows per LDS round trip
             const uint4 cc[2] = {c[k], c[k + 1]};
             uint4 dd[2] = {d[k], d[k + 1]};
             dec_cbc<2>(lds, lo, dk0, cc, dd);
             d[k] = dd[0];
             d[k + 1] = dd[1];
         }
+#else
+        dec_cbc<R>(lds, lo, dk0, c, d);  // all R rows per LDS round trip (A/B: ~1% over 2 rows)
+#endif
     } else {
 #pragma unroll
         for (int k = 0; k < R; k++) {
@@ -393,7 +532,8 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
                 const uint32_t ku = __builtin_amdgcn_readlane(kid, __builtin_ctzll(m));
                 if (pending && kid == ku) {
                     pending = false;
-                    const uint32_t* __restrict__ dk = a.keys.table + (uint64_t)ku * kSchedWords + 44;
+                    uint32_t dk[44];
+                    load_sched(a.keys.table + (uint64_t)ku * kSchedWords + 44, dk);
                     const uint4 cc[1] = {c[k]};
                     uint4 dd[1] = {d[k]};
                     dec_cbc<1>(lds, lo, dk, cc, dd);
@@ -434,14 +574,16 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     ps.bpos = (uint32_t)(begin - ps.bp * a.bpp.d);
     uint4 carry = make_uint4(0, 0, 0, 0);  // C[base-1]
     if (ps.bpos != 0) carry = a.boundary ? a.boundary[wave] : reinterpret_cast<const uint4*>(a.in)[begin - 1];
+    uint32_t dk0[44];
+    if (!KEYED) load_sched(a.keys.table + 44, dk0);
     uint64_t base = begin;
     for (; base + 64 * R <= end; base += 64 * R) {
-        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry);
+        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0);
         ps.bpos += a.step_r;
         ps.bp += a.step_q;
         if (ps.bpos >= a.bpp.d) { ps.bpos -= a.bpp.d; ps.bp++; }
     }
-    if (base < end) flat_step<KEYED, BIG, false>(a, lds, lo, lane, base, end, ps, carry);
+    if (base < end) flat_step<KEYED, BIG, false>(a, lds, lo, lane, base, end, ps, carry, dk0);
 }
 
 // ---- CBC decrypt, ragged batch: one wave per payload ----------------------
@@ -469,7 +611,8 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
             kid = a.keys.nkeys - 1;
         }
         kid = __builtin_amdgcn_readfirstlane(kid);
-        const uint32_t* __restrict__ dk = a.keys.table + (uint64_t)kid * kSchedWords + 44;
+        uint32_t dk[44];
+        load_sched(a.keys.table + (uint64_t)kid * kSchedWords + 44, dk);
         uint4 carry = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
         if (nb == 0 && a.iv_out && lane == 0) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = carry;  // chain unchanged
         for (uint32_t base = 0; base < nb; base += 64 * R) {
@@ -603,6 +746,14 @@ __global__ void k_digest(const uint64_t* buf, uint64_t nwords, unsigned long lon
 hipError_t launch_encrypt(const EncArgs& a, int grid, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
     const bool ragged = a.offsets != nullptr;
+#if CYAES_ENC2
+    if (!ragged && !keyed) {
+        const uint64_t want = (a.npayloads + 2 * kEnc2Threads - 1) / (2 * kEnc2Threads);
+        const int g2 = (int)(want < (uint64_t)grid ? want : (uint64_t)grid);
+        hipLaunchKernelGGL(k_encrypt2, dim3(g2 > 0 ? g2 : 1), dim3(kEnc2Threads), 0, stream, a);
+        return hipGetLastError();
+    }
+#endif
     const dim3 g(grid), b(kEncThreads);
     if (ragged && keyed) hipLaunchKernelGGL((k_encrypt<true, true>), g, b, 0, stream, a);
     else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false>), g, b, 0, stream, a);

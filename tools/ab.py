@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""tools/ab.py -- interleaved A/B timing of libcyaes.so variants in ONE process
+(MI355X_MICROARCH.md: never rank builds by timings from different runs/devices).
+
+usage: python tools/ab.py build/variants/a.so build/variants/b.so [--rounds 6] [--payloads N]
+Each round runs every variant's encrypt and decrypt once on the same config-C
+buffers; prints per-variant median/min ms per kernel and checks the outputs agree.
+"""
+import argparse
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--payloads", type=int, default=262144)
+    ap.add_argument("--payload-bytes", type=int, default=65536)
+    args = ap.parse_args()
+    import torch
+    import cyclone_amd as ca
+
+    n, pb = args.payloads, args.payload_bytes
+    nbytes = n * pb
+    ctxs = []
+    for path in args.libs:
+        lib = ca.load_library(os.path.abspath(path))
+        c = ca.GpuContext(0, lib=lib)
+        c.set_keys(bytes(range(16)))
+        ctxs.append(c)
+    pt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    ct = torch.empty_like(pt)
+    rt = torch.empty_like(pt)
+    ctxs[0].fill_synthetic(pt, 0, n, pb, 0x5EEDC1C1)
+    s = torch.cuda.current_stream()
+    times = {p: {"enc": [], "dec": []} for p in args.libs}
+    digests = {}
+    for r in range(args.rounds + 1):
+        for path, c in zip(args.libs, ctxs):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record(s)
+            c.encrypt_uniform(pt, ct, n, pb, stream=s.cuda_stream)
+            e[1].record(s)
+            c.decrypt_uniform(ct, rt, n, pb, stream=s.cuda_stream)
+            e[2].record(s)
+            torch.cuda.synchronize()
+            if r == 0:  # warm-up round; check outputs
+                digests[path] = (c.digest(ct, nbytes), c.digest(rt, nbytes))
+                continue
+            times[path]["enc"].append(e[0].elapsed_time(e[1]))
+            times[path]["dec"].append(e[1].elapsed_time(e[2]))
+    ref = digests[args.libs[0]]
+    for path in args.libs:
+        t = times[path]
+        print("%-40s enc med %.3f min %.3f | dec med %.3f min %.3f | %s" % (
+            os.path.basename(path), statistics.median(t["enc"]), min(t["enc"]), statistics.median(t["dec"]),
+            min(t["dec"]), "same-output" if digests[path] == ref else "OUTPUT DIFFERS"))
+
+
+if __name__ == "__main__":
+    main()

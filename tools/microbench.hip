@@ -113,6 +113,69 @@ __global__ __launch_bounds__(1024, 1) void k_mix(uint32_t* out, int iters, Clk* 
     }
 }
 
+// LDS peak: one v_perm per 4 conflict-free ds_read_b32 (offsets 0/64/128/192)
+// and one xor3 per 2 reads, so VALU cannot bind.  B64: ds_read_b64 instead.
+template <bool B64>
+__global__ __launch_bounds__(1024, 1) void k_ldspeak(uint32_t* out, int iters, Clk* clk) {
+    __shared__ uint32_t lds[24576];  // 96 KiB: one workgroup per CU
+    for (int i = threadIdx.x; i < 24576; i += blockDim.x) lds[i] = i * 2654435761u;
+    __syncthreads();
+    const uint32_t lo = (threadIdx.x & 31u) << (B64 ? 3 : 2);
+    uint32_t s[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) s[j] = (threadIdx.x * 7919u + j * 104729u) | 1;
+    unsigned long long t0 = 0, r0 = 0;
+    if (threadIdx.x == 0) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    const char* base = reinterpret_cast<const char*>(lds);
+    for (int it = 0; it < iters; it++) {
+        uint32_t a[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) a[j] = __builtin_amdgcn_perm(s[j], lo, 0x0C0C0400u + (j << 8));
+        if (B64) {
+            uint2 v[8];
+            asm volatile(
+                "ds_read_b64 %0, %8\n\tds_read_b64 %1, %8 offset:256\n\t"
+                "ds_read_b64 %2, %9\n\tds_read_b64 %3, %9 offset:256\n\t"
+                "ds_read_b64 %4, %10\n\tds_read_b64 %5, %10 offset:256\n\t"
+                "ds_read_b64 %6, %11\n\tds_read_b64 %7, %11 offset:256\n\ts_waitcnt lgkmcnt(0)"
+                : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+                  "=&v"(v[7])
+                : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+                : "memory");
+#pragma unroll
+            for (int j = 0; j < 4; j++) s[j] = xor3(s[j], v[2 * j].x ^ v[2 * j].y, v[2 * j + 1].x ^ v[2 * j + 1].y);
+        } else {
+            uint32_t v[16];
+            asm volatile(
+                "ds_read_b32 %0, %16\n\tds_read_b32 %1, %16 offset:128\n\tds_read_b32 %2, %16 offset:256\n\t"
+                "ds_read_b32 %3, %16 offset:384\n\t"
+                "ds_read_b32 %4, %17\n\tds_read_b32 %5, %17 offset:128\n\tds_read_b32 %6, %17 offset:256\n\t"
+                "ds_read_b32 %7, %17 offset:384\n\t"
+                "ds_read_b32 %8, %18\n\tds_read_b32 %9, %18 offset:128\n\tds_read_b32 %10, %18 offset:256\n\t"
+                "ds_read_b32 %11, %18 offset:384\n\t"
+                "ds_read_b32 %12, %19\n\tds_read_b32 %13, %19 offset:128\n\tds_read_b32 %14, %19 offset:256\n\t"
+                "ds_read_b32 %15, %19 offset:384\n\ts_waitcnt lgkmcnt(0)"
+                : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+                  "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]), "=&v"(v[12]), "=&v"(v[13]),
+                  "=&v"(v[14]), "=&v"(v[15])
+                : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+                : "memory");
+#pragma unroll
+            for (int j = 0; j < 4; j++) s[j] = xor3(s[j], xor3(v[4 * j], v[4 * j + 1], v[4 * j + 2]), v[4 * j + 3]);
+        }
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s[0] ^ s[1] ^ s[2] ^ s[3];
+    if (threadIdx.x == 0) {
+        clk[blockIdx.x].t0 = t0;
+        clk[blockIdx.x].r0 = r0;
+        clk[blockIdx.x].t1 = __builtin_amdgcn_s_memtime();
+        clk[blockIdx.x].r1 = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // VALU issue: 8 independent chains x 8 unrolled ops of one kind.
 template <int OP>
 __global__ __launch_bounds__(1024, 1) void k_valu(uint32_t* out, int iters, Clk* clk) {
@@ -220,6 +283,9 @@ int main() {
     run("lds_gather_x3", k_lds<3>, 1024, it, 16, "lookups", cus, d_out, d_clk);
     run("lds_gather_x0_8waves", k_lds<0>, 512, it, 16, "lookups", cus, d_out, d_clk);
     run("lds_gather_x0_4waves", k_lds<0>, 256, it, 16, "lookups", cus, d_out, d_clk);
+    run("lds_peak_b32", k_ldspeak<false>, 1024, it, 16, "ds_read_b32 lanes", cus, d_out, d_clk);
+    run("lds_peak_b64", k_ldspeak<true>, 1024, it, 8, "ds_read_b64 lanes", cus, d_out, d_clk);
+    run("lds_peak_b32_8w", k_ldspeak<false>, 512, it, 16, "ds_read_b32 lanes", cus, d_out, d_clk);
     run("mix_vmem0", k_mix<0>, 1024, it, 16, "lookups", cus, d_out, d_clk);
     run("mix_vmem2", k_mix<2>, 1024, it, 16, "lookups", cus, d_out, d_clk);
     run("mix_vmem4", k_mix<4>, 1024, it, 16, "lookups", cus, d_out, d_clk);
