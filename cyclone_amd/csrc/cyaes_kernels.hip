@@ -298,10 +298,20 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                 const uint4* src = reinterpret_cast<const uint4*>(a.in + off);
                 uint4* dst = reinterpret_cast<uint4*>(a.out + off);
                 uint32_t i = 0;
-                for (; i + 8 <= nb; i += 8) {
-                    uint4 b[8];
+                uint4 b[8];
+                if (nb >= 8) {
 #pragma unroll
-                    for (int j = 0; j < 8; j++) b[j] = src[i + j];
+                    for (int j = 0; j < 8; j++) b[j] = src[j];
+                }
+                for (; i + 8 <= nb; i += 8) {
+#if !CYAES_NO_PREFETCH  // A/B: -8% encrypt time vs loading at the top of the chunk
+                    uint4 bn[8];  // next chunk's loads in flight during this chunk's rounds
+                    const bool more = i + 16 <= nb;
+                    if (more) {
+#pragma unroll
+                        for (int j = 0; j < 8; j++) bn[j] = src[i + 8 + j];
+                    }
+#endif
 #pragma unroll
                     for (int j = 0; j < 8; j++) {
                         uint32_t s0 = xor3(c.x, b[j].x, ek[0]), s1 = xor3(c.y, b[j].y, ek[1]);
@@ -312,6 +322,17 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                     }
 #pragma unroll
                     for (int j = 0; j < 8; j++) dst[i + j] = b[j];
+#if CYAES_NO_PREFETCH
+                    if (i + 16 <= nb) {
+#pragma unroll
+                        for (int j = 0; j < 8; j++) b[j] = src[i + 8 + j];
+                    }
+#else
+                    if (more) {
+#pragma unroll
+                        for (int j = 0; j < 8; j++) b[j] = bn[j];
+                    }
+#endif
                 }
                 for (; i < nb; i++) {
                     const uint4 v = src[i];
@@ -443,15 +464,13 @@ __device__ __forceinline__ void flat_position(const DecArgs& a, FlatPos ps, uint
 // One step of R rows at block `base`.  FULL: all 64*R blocks are in range
 // (every step but possibly the batch's last), so loads and stores are
 // unguarded and use immediate offsets off one lane pointer.
-template <bool KEYED, bool BIG, bool FULL>
-__device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, uint32_t lo, uint32_t lane,
-                                           uint64_t base, uint64_t end, FlatPos ps, uint4 carry,
-                                           const uint32_t (&dk0)[44]) {
+// Loads the R rows of the step at `base` (c) and each block's predecessor (pv).
+template <bool FULL>
+__device__ __forceinline__ void flat_load(const DecArgs& a, uint32_t lane, uint64_t base, uint64_t end,
+                                          uint4 (&c)[kDecRows], uint4 (&pv)[kDecRows]) {
     constexpr int R = kDecRows;
     const uint4* __restrict__ in = reinterpret_cast<const uint4*>(a.in);
-    uint4* out = reinterpret_cast<uint4*>(a.out);
     const uint64_t back = lane ? 1u : 0u;  // lane 0 reads its own block (replaced by carry)
-    uint4 c[R], pv[R];
     if (FULL) {
         const uint64_t g0 = base + lane;
 #pragma unroll
@@ -467,6 +486,15 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
             pv[k] = in[g - ((k == 0) ? back : 1u)];
         }
     }
+}
+
+template <bool KEYED, bool BIG, bool FULL>
+__device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, uint32_t lo, uint32_t lane,
+                                           uint64_t base, uint64_t end, FlatPos ps, uint4 carry,
+                                           const uint32_t (&dk0)[44], const uint4 (&c)[kDecRows],
+                                           uint4 (&pv)[kDecRows]) {
+    constexpr int R = kDecRows;
+    uint4* out = reinterpret_cast<uint4*>(a.out);
     if (lane == 0) pv[0] = carry;
     if (a.inplace) drain_loads();
     // Chain restarts at payload starts inside this step.
@@ -577,13 +605,31 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     uint32_t dk0[44];
     if (!KEYED) load_sched(a.keys.table + 44, dk0);
     uint64_t base = begin;
+    uint4 c[R], pv[R];
+    if (base + 64 * R <= end) flat_load<true>(a, lane, base, end, c, pv);
     for (; base + 64 * R <= end; base += 64 * R) {
-        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0);
+#if !CYAES_DEC_PREFETCH  // A/B (tools/ab.py): prefetching the next step costs ~1% here
+        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0, c, pv);
+        if (base + 128 * R <= end) flat_load<true>(a, lane, base + 64 * R, end, c, pv);
+#else
+        // Issue the next step's loads before this step's rounds.
+        uint4 cn[R], pvn[R];
+        const bool more = base + 128 * R <= end;
+        if (more) flat_load<true>(a, lane, base + 64 * R, end, cn, pvn);
+        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0, c, pv);
+        if (more) {
+#pragma unroll
+            for (int k = 0; k < R; k++) { c[k] = cn[k]; pv[k] = pvn[k]; }
+        }
+#endif
         ps.bpos += a.step_r;
         ps.bp += a.step_q;
         if (ps.bpos >= a.bpp.d) { ps.bpos -= a.bpp.d; ps.bp++; }
     }
-    if (base < end) flat_step<KEYED, BIG, false>(a, lds, lo, lane, base, end, ps, carry, dk0);
+    if (base < end) {
+        flat_load<false>(a, lane, base, end, c, pv);
+        flat_step<KEYED, BIG, false>(a, lds, lo, lane, base, end, ps, carry, dk0, c, pv);
+    }
 }
 
 // ---- CBC decrypt, ragged batch: one wave per payload ----------------------
