@@ -321,7 +321,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                         b[j] = c;
                     }
 #pragma unroll
-                    for (int j = 0; j < 8; j++) dst[i + j] = b[j];
+                    for (int j = 0; j < 8; j++) dst[i + j] = b[j];  // (nt stores measured 3.6x slower)
 #if CYAES_NO_PREFETCH
                     if (i + 16 <= nb) {
 #pragma unroll
