@@ -253,7 +253,55 @@ __device__ __forceinline__ void load_sched(const uint32_t* p, uint32_t (&k)[44])
     }
 }
 
+// Progress-feedback wave priority.  The SQ serves the oldest ready wave
+// first, so under LDS saturation the 16 waves of a workgroup would finish
+// staggered (measured with CYAES_CLOCK_PROBE: wave 0 at ~55 % of the kernel
+// time, wave 15 at 100 %) and the tail would run with 4 waves/CU, far below
+// the LDS gather peak.  Each wave publishes its step count to an LDS max; a
+// wave trailing the block's leader by d steps runs at priority min(d / div, 3).
+// The waves then finish together (probe: within 1 %); -7.5 % encrypt and -8 %
+// decrypt time on config C (tools/ab.py).  Lockstepping the waves with
+// s_barrier instead was measured worse (encrypt +5 %, decrypt -4 %).  CYAES_NO_PRIO=1 builds without it.
+__device__ __forceinline__ void prio_feedback(uint32_t* lead, uint32_t step, uint32_t div) {
+#if !CYAES_NO_PRIO
+    // first active lane publishes (lane 0 may be masked off in a waterfall)
+    const uint32_t fl = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
+    uint32_t m = 0;
+    if (__lane_id() == fl) m = atomicMax(lead, step);
+    m = __builtin_amdgcn_readfirstlane(m);
+    step = __builtin_amdgcn_readfirstlane(step);  // keeps d scalar: the branches below must be uniform jumps,
+    const uint32_t d = m > step ? (m - step) / div : 0u;  // not exec-masked (s_setprio ignores exec)
+    if (d >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (d == 2) __builtin_amdgcn_s_setprio(2);
+    else if (d == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#endif
+}
+constexpr uint32_t kEncPrioDiv = 4;  // steps = 8-block chunks (A/B: 1, 2, 4, 8 -> 4 best)
+constexpr uint32_t kDecPrioDiv = 8;  // steps = 64*kDecRows-block rows (A/B: 4, 8, 16 -> 8)
+
+
 __device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kIv2, kIv3); }
+
+#if CYAES_CLOCK_PROBE
+// Variant builds only (make variant DEFS=-DCYAES_CLOCK_PROBE=1): shader clock
+// of a few waves over the kernel body, s_memtime (SCLK) vs s_memrealtime (100 MHz).
+struct ClockProbe {
+    uint64_t t0, r0;
+    __device__ ClockProbe() : t0(__builtin_amdgcn_s_memtime()), r0(__builtin_amdgcn_s_memrealtime()) {}
+    __device__ ~ClockProbe() {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0 && (blockIdx.x == 0 || blockIdx.x == 100)) {
+            const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804), xcc = __builtin_amdgcn_s_getreg(0xF814);
+            printf("clockprobe block %u wave %u xcc %u hwid %08x r0 %llu r1 %llu cycles %llu\n", blockIdx.x, threadIdx.x >> 6, xcc, hw,
+                   (unsigned long long)r0, (unsigned long long)r1, (unsigned long long)(t1 - t0));
+        }
+    }
+};
+#define CLOCK_PROBE ClockProbe clock_probe_
+#else
+#define CLOCK_PROBE
+#endif
 
 // In-place batches: every load of a step must have returned before the step's
 // first store (a lane's previous-block load reads a neighbour's block).
@@ -265,7 +313,11 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
     fill_region(lds_words, a.tables, a.tables + 256, kEncThreads);
     fill_region(lds_words + 16384, a.tables + 512, a.tables + 768, kEncThreads);
+    __shared__ uint32_t lead;  // prio_feedback
+    if (threadIdx.x == 0) lead = 0;
+    uint32_t prog = 0;
     __syncthreads();
+    CLOCK_PROBE;
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
@@ -312,6 +364,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                         for (int j = 0; j < 8; j++) bn[j] = src[i + 8 + j];
                     }
 #endif
+                    prio_feedback(&lead, ++prog, kEncPrioDiv);
 #pragma unroll
                     for (int j = 0; j < 8; j++) {
                         uint32_t s0 = xor3(c.x, b[j].x, ek[0]), s1 = xor3(c.y, b[j].y, ek[1]);
@@ -588,7 +641,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
     fill_region(lds_words, a.tables, a.tables + 256, kDecThreads);
     fill_region(lds_words + 16384, a.tables + 512, nullptr, kDecThreads);
+    __shared__ uint32_t lead;  // prio_feedback
+    if (threadIdx.x == 0) lead = 0;
+    uint32_t prog = 0;
     __syncthreads();
+    CLOCK_PROBE;
     const uint64_t wave =
         (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t begin = wave * a.blocks_per_wave;
@@ -622,6 +679,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
             for (int k = 0; k < R; k++) { c[k] = cn[k]; pv[k] = pvn[k]; }
         }
 #endif
+        prio_feedback(&lead, ++prog, kDecPrioDiv);
         ps.bpos += a.step_r;
         ps.bp += a.step_q;
         if (ps.bpos >= a.bpp.d) { ps.bpos -= a.bpp.d; ps.bp++; }
@@ -638,6 +696,9 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
     fill_region(lds_words, a.tables, a.tables + 256, kDecThreads);
     fill_region(lds_words + 16384, a.tables + 512, nullptr, kDecThreads);
+    __shared__ uint32_t lead;  // prio_feedback
+    if (threadIdx.x == 0) lead = 0;
+    uint32_t prog = 0;
     __syncthreads();
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
@@ -662,6 +723,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         uint4 carry = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
         if (nb == 0 && a.iv_out && lane == 0) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = carry;  // chain unchanged
         for (uint32_t base = 0; base < nb; base += 64 * R) {
+            prio_feedback(&lead, ++prog, kDecPrioDiv);
             uint4 c[R], pv[R];
 #pragma unroll
             for (int k = 0; k < R; k++) {
@@ -676,16 +738,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                 const uint32_t g = base + 64 * k + lane;
                 if (a.iv_out && g + 1 == nb) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
             }
+            dec_cbc<R>(lds, lo, dk, c, pv);
 #pragma unroll
-            for (int k = 0; k < R; k += 2) {
-                const uint4 cc[2] = {c[k], c[k + 1]};
-                uint4 dd[2] = {pv[k], pv[k + 1]};
-                dec_cbc<2>(lds, lo, dk, cc, dd);
-#pragma unroll
-                for (int n = 0; n < 2; n++) {
-                    const uint32_t g = base + 64 * (k + n) + lane;
-                    if (g < nb) out[g] = dd[n];
-                }
+            for (int k = 0; k < R; k++) {
+                const uint32_t g = base + 64 * k + lane;
+                if (g < nb) out[g] = pv[k];
             }
             carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
         }
