@@ -27,10 +27,12 @@
 //    present in a wave, normally one).
 //  * Encrypt (serial CBC): one lane = one payload chain, 8 blocks (128 B, one
 //    full line per lane) loaded per step.
-//  * Decrypt (block-parallel): one lane = one 16-B block, two rows decrypted
-//    together, each wave-instruction loads 1 KiB contiguous; the previous ciphertext block is a second load at
-//    offset -16 (an L1/L2 hit), the wave's chain across steps is carried in
-//    registers.
+//  * Decrypt (block-parallel): one lane = one 16-B block, four rows decrypted
+//    together, each wave-instruction loads 1 KiB contiguous; the previous
+//    ciphertext block comes from the neighbour lane (DPP wave_shr:1), the
+//    wave's chain across rows and steps through readlane 63.
+//  * Waves of a workgroup are kept level by progress-feedback priority
+//    (prio_feedback), so none runs a starved tail.
 #include "cyaes_internal.h"
 
 namespace cyaes {
@@ -284,23 +286,28 @@ constexpr uint32_t kDecPrioDiv = 8;  // steps = 64*kDecRows-block rows (A/B: 4, 
 __device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kIv2, kIv3); }
 
 #if CYAES_CLOCK_PROBE
-// Variant builds only (make variant DEFS=-DCYAES_CLOCK_PROBE=1): shader clock
-// of a few waves over the kernel body, s_memtime (SCLK) vs s_memrealtime (100 MHz).
+// Variant builds only (make variant DEFS=-DCYAES_CLOCK_PROBE=1): per-wave
+// shader cycles (s_memtime) and wall ticks (s_memrealtime, 100 MHz per
+// tools/clockcal.hip) over the kernel body, summed per kernel kind into
+// g_probe and read by cyaes_debug_probe() (tools/ab.py prints the clock).
+__device__ unsigned long long g_probe[2][4];  // [enc, dec] x {cycles, ticks, waves, max ticks}
 struct ClockProbe {
     uint64_t t0, r0;
-    __device__ ClockProbe() : t0(__builtin_amdgcn_s_memtime()), r0(__builtin_amdgcn_s_memrealtime()) {}
+    int kind;
+    __device__ explicit ClockProbe(int k) : t0(__builtin_amdgcn_s_memtime()), r0(__builtin_amdgcn_s_memrealtime()), kind(k) {}
     __device__ ~ClockProbe() {
         const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        if ((threadIdx.x & 63) == 0 && (blockIdx.x == 0 || blockIdx.x == 100)) {
-            const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804), xcc = __builtin_amdgcn_s_getreg(0xF814);
-            printf("clockprobe block %u wave %u xcc %u hwid %08x r0 %llu r1 %llu cycles %llu\n", blockIdx.x, threadIdx.x >> 6, xcc, hw,
-                   (unsigned long long)r0, (unsigned long long)r1, (unsigned long long)(t1 - t0));
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&g_probe[kind][0], (unsigned long long)(t1 - t0));
+            atomicAdd(&g_probe[kind][1], (unsigned long long)(r1 - r0));
+            atomicAdd(&g_probe[kind][2], 1ull);
+            atomicMax(&g_probe[kind][3], (unsigned long long)(r1 - r0));
         }
     }
 };
-#define CLOCK_PROBE ClockProbe clock_probe_
+#define CLOCK_PROBE(k) ClockProbe clock_probe_(k)
 #else
-#define CLOCK_PROBE
+#define CLOCK_PROBE(k)
 #endif
 
 // In-place batches: every load of a step must have returned before the step's
@@ -317,7 +324,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     if (threadIdx.x == 0) lead = 0;
     uint32_t prog = 0;
     __syncthreads();
-    CLOCK_PROBE;
+    CLOCK_PROBE(0);
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
@@ -517,7 +524,16 @@ __device__ __forceinline__ void flat_position(const DecArgs& a, FlatPos ps, uint
 // One step of R rows at block `base`.  FULL: all 64*R blocks are in range
 // (every step but possibly the batch's last), so loads and stores are
 // unguarded and use immediate offsets off one lane pointer.
-// Loads the R rows of the step at `base` (c) and each block's predecessor (pv).
+// v (lane l-1) for lanes 1..63, old for lane 0: DPP wave_shr:1.
+__device__ __forceinline__ uint32_t shr1(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint4 shr1(uint4 v, uint4 old) {
+    return make_uint4(shr1(v.x, old.x), shr1(v.y, old.y), shr1(v.z, old.z), shr1(v.w, old.w));
+}
+
+// Loads the R rows of the step at `base` (c); partial steps also load each
+// block's predecessor (pv), full steps take it from the neighbour lane.
 template <bool FULL>
 __device__ __forceinline__ void flat_load(const DecArgs& a, uint32_t lane, uint64_t base, uint64_t end,
                                           uint4 (&c)[kDecRows], uint4 (&pv)[kDecRows]) {
@@ -528,9 +544,7 @@ __device__ __forceinline__ void flat_load(const DecArgs& a, uint32_t lane, uint6
         const uint64_t g0 = base + lane;
 #pragma unroll
         for (int k = 0; k < R; k++) c[k] = in[g0 + 64 * k];
-        pv[0] = in[g0 - back];
-#pragma unroll
-        for (int k = 1; k < R; k++) pv[k] = in[g0 + 64 * k - 1];
+        // pv comes from the neighbour lane in flat_step (DPP), not from memory
     } else {  // last, partial step of the batch: clamp reads into range
 #pragma unroll
         for (int k = 0; k < R; k++) {
@@ -548,8 +562,20 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
                                            uint4 (&pv)[kDecRows]) {
     constexpr int R = kDecRows;
     uint4* out = reinterpret_cast<uint4*>(a.out);
-    if (lane == 0) pv[0] = carry;
-    if (a.inplace) drain_loads();
+    if (FULL) {
+        // Predecessor blocks from the neighbour lane (DPP wave_shr:1), lane 0's
+        // from the row before (or the carry): no second load of C[i-1]
+        // (A/B: -4.8 % decrypt time vs the load at offset -16).  Every load of
+        // the step is then the lane's own block, which its store needs anyway,
+        // so in-place steps need no drain.
+        pv[0] = shr1(c[0], carry);
+#pragma unroll
+        for (int k = 1; k < R; k++)
+            pv[k] = shr1(c[k], make_uint4(rl63(c[k - 1].x), rl63(c[k - 1].y), rl63(c[k - 1].z), rl63(c[k - 1].w)));
+    } else {
+        if (lane == 0) pv[0] = carry;
+        if (a.inplace) drain_loads();  // pv loads read neighbours' blocks
+    }
     // Chain restarts at payload starts inside this step.
     if (BIG) {
         const uint32_t fo = ps.bpos == 0 ? 0u : a.bpp.d - ps.bpos;  // offset of the payload start, if < 64R
@@ -645,7 +671,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     if (threadIdx.x == 0) lead = 0;
     uint32_t prog = 0;
     __syncthreads();
-    CLOCK_PROBE;
+    CLOCK_PROBE(1);
     const uint64_t wave =
         (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t begin = wave * a.blocks_per_wave;
@@ -706,8 +732,6 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * (kDecThreads / 64);
     const uint64_t wave0 =
         (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool inplace = a.inplace != 0;
-
     for (uint64_t p = wave0; p < a.npayloads; p += nwaves) {
         const uint4* in = reinterpret_cast<const uint4*>(a.in + a.offsets[p]);
         uint4* out = reinterpret_cast<uint4*>(a.out + a.offsets[p]);
@@ -728,11 +752,14 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 const uint32_t g = base + 64 * k + lane;
-                const bool valid = g < nb;
-                c[k] = valid ? in[g] : make_uint4(0, 0, 0, 0);
-                pv[k] = (valid && (k > 0 || lane > 0)) ? in[g - 1] : carry;
+                c[k] = g < nb ? in[g] : make_uint4(0, 0, 0, 0);
             }
-            if (inplace) drain_loads();
+            // predecessors from the neighbour lane (as k_decrypt_flat): no loads of
+            // other lanes' blocks, so in-place needs no drain
+            pv[0] = shr1(c[0], carry);
+#pragma unroll
+            for (int k = 1; k < R; k++)
+                pv[k] = shr1(c[k], make_uint4(rl63(c[k - 1].x), rl63(c[k - 1].y), rl63(c[k - 1].z), rl63(c[k - 1].w)));
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 const uint32_t g = base + 64 * k + lane;
@@ -919,3 +946,12 @@ hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long
 }
 
 }  // namespace cyaes
+
+#if CYAES_CLOCK_PROBE
+// Reads and clears the probe sums: out[8] = g_probe (enc, dec).
+extern "C" int cyaes_debug_probe(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cyaes::g_probe), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    static const unsigned long long zero[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(cyaes::g_probe), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif

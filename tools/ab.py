@@ -39,6 +39,7 @@ def main():
     ctxs[0].fill_synthetic(pt, 0, n, pb, 0x5EEDC1C1)
     s = torch.cuda.current_stream()
     times = {p: {"enc": [], "dec": []} for p in args.libs}
+    probes = {}
     digests = {}
     for r in range(args.rounds + 1):
         for path, c in zip(args.libs, ctxs):
@@ -51,7 +52,9 @@ def main():
             torch.cuda.synchronize()
             if r == 0:  # warm-up round; check outputs
                 digests[path] = (c.digest(ct, nbytes), c.digest(rt, nbytes))
+                probe(c, None)
                 continue
+            probe(c, probes.setdefault(path, []))
             times[path]["enc"].append(e[0].elapsed_time(e[1]))
             times[path]["dec"].append(e[1].elapsed_time(e[2]))
     ref = digests[args.libs[0]]
@@ -60,6 +63,23 @@ def main():
         print("%-40s enc med %.3f min %.3f | dec med %.3f min %.3f | %s" % (
             os.path.basename(path), statistics.median(t["enc"]), min(t["enc"]), statistics.median(t["dec"]),
             min(t["dec"]), "same-output" if digests[path] == ref else "OUTPUT DIFFERS"))
+        for kind, v in zip(("enc", "dec"), zip(*probes.get(path, []))):
+            cyc, tick, waves, tmax = (sum(x[i] for x in v) for i in range(4))
+            if waves:
+                print("    %s clock %.3f GHz, mean wave %.3f ms, max wave %.3f ms (per launch)" % (
+                    kind, cyc / tick * 0.1, tick / waves / 1e5, tmax / len(v) / 1e5))
+
+
+def probe(ctx, sink):
+    """Reads (and clears) the CYAES_CLOCK_PROBE sums of a variant build, if it has them."""
+    import ctypes
+    fn = getattr(ctx._lib, "cyaes_debug_probe", None)
+    if fn is None:
+        return
+    buf = (ctypes.c_ulonglong * 8)()
+    fn(buf)
+    if sink is not None:
+        sink.append((tuple(buf[0:4]), tuple(buf[4:8])))
 
 
 if __name__ == "__main__":
