@@ -10,9 +10,6 @@ namespace cyaes {
 // Device key schedule: the reference's m_Ke / m_Kd words (cyr_rijndael.h:50,52)
 // byte-swapped to little-endian so a dwordx4 load of a block is directly the
 // cipher state.  88 words = 352 B per key, ek at [0,44), dk at [44,88).
-// Decryption round keys of rounds 1..9 are stored rotated right by 8 bits:
-// the decrypt kernels fold the key into the rotated half of each column
-// (DESIGN.md §3.2).  Encryption keys are plain.
 constexpr int kSchedWords = 88;
 
 // LDS images.  A row is 256 B: word A[x] in slots 0..31 and
@@ -20,10 +17,11 @@ constexpr int kSchedWords = 88;
 // l%32 and every T-table gather is conflict-free.  The address of (x, lane)
 // is one v_perm_b32: x << 8 | (lane & 31) << 2.
 //   encrypt: region 0 A = TL1, B = TL2; region 1 (+64 KiB) A = TL3, B = TL4.
-//   decrypt: region 0 A = TL5, B = TL7; region 1 A = Si x 0x01010101.
+//   decrypt: region 0 A = TL5, B = TL6; region 1 A = TL7, B = TL8; then, at
+//            128 KiB, Si x 0x01010101 in 128-B rows (32 slots), 32 KiB.
 // Region 1 is addressed through byte 2 of the lane offset register (= 1).
 constexpr int kEncLdsWords = 32768;  // 128 KiB
-constexpr int kDecLdsWords = 32768;  // 128 KiB
+constexpr int kDecLdsWords = 40960;  // 160 KiB: the whole LDS of a CU
 constexpr int kEncTableWords = 1024; // TL1, TL2, TL3, TL4
 constexpr int kDecTableWords = 768;  // TL5[256], TL7[256], SiW[256]
 // Byte offsets inside the device table buffer.
@@ -32,7 +30,7 @@ constexpr int kDecTableOff = kEncTableWords * 4;
 constexpr int kSboxOff = kDecTableOff + kDecTableWords * 4;
 constexpr int kTablesBytes = kSboxOff + 256;
 
-// Workgroup shapes: 16 waves x 1 WG/CU (128 KiB LDS) for both directions.
+// Workgroup shapes: 16 waves x 1 WG/CU (128 / 160 KiB LDS) for both directions.
 constexpr int kEncThreads = 1024;
 constexpr int kEncWgPerCu = 1;
 constexpr int kDecThreads = 1024;

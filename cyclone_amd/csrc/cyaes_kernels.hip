@@ -16,12 +16,10 @@
 //    the lane-offset register, still one v_perm_b32.
 //    Encrypt keeps all four T-tables (TL1|TL2, TL3|TL4): a column is
 //        xor3(TL1[b0], TL2[b1], xor3(TL3[b2], TL4[b3], k)).
-//    Decrypt keeps TL5|TL7 and Si; TL6/TL8 are rotl8 of those and a column
-//    needs one rotation because rotation distributes over XOR:
-//        col = TL5[b0] ^ TL7[b2] ^ rotl8(TL5[b1] ^ TL7[b3] ^ rotr8(k)),
-//    with the decryption round keys of rounds 1..9 stored pre-rotated.
+//    Decrypt fills the whole 160 KiB: TL5|TL6, TL7|TL8 and a 32 KiB Si image
+//    with 128-B rows (address = perm >> 1), so its columns have the same form.
 //    The last round's S-box bytes come from TL1/TL3 bytes (encrypt) or the
-//    Si x 0x01010101 region (decrypt), merged with v_bfi_b32 / v_perm_b32.
+//    Si x 0x01010101 image (decrypt), merged with v_bfi_b32 / v_perm_b32.
 //  * Round keys are wave-uniform and live in SGPRs (s_load from the key table;
 //    a per-payload key index is handled by a waterfall over the distinct keys
 //    present in a wave, normally one).
@@ -83,17 +81,6 @@ __device__ __forceinline__ uint32_t fastdiv(uint32_t n, const Fastdiv& f) {
     const uint64_t lo = (uint64_t)(uint32_t)f.M * n;
     const uint64_t hi = (f.M >> 32) * n;
     return (uint32_t)((hi + (lo >> 32)) >> 32);
-}
-
-// Decrypt middle-round column.  x0..x3 supply bytes b0..b3; A-table reads
-// for b0/b1, B-table reads for b2/b3; kr = rotr8(round key word).
-__device__ __forceinline__ uint32_t dcol(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
-                                         uint32_t x3, uint32_t kr) {
-    const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));
-    const uint32_t l1 = ld(lds, addr(x1, lo, kSel1));
-    const uint32_t l2 = ld(lds + kHalfB, addr(x2, lo, kSel2));
-    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, kSel3));
-    return xor3(l0, l2, rotl8(xor3(l1, l3, kr)));
 }
 
 // Encrypt middle-round column: all four T-tables resident, no rotation.
@@ -174,18 +161,52 @@ __device__ __forceinline__ void enc_block(const char* lds, uint32_t lo, const ui
 }
 
 // ---- decryption (_decryptBlock, cyr_rijndael.cpp:708-774) -----------------
-// Region 0 rows: A = TL5 (LE bytes 14s,9s,13s,11s), B = TL7 = rotl16(TL5);
-// TL6/TL8 = rotl8.  Column j takes b0(u_j), b1(u_j-1), b2(u_j-2), b3(u_j-3)
-// (inverse ShiftRows, cyr_rijndael.cpp:731-746).  Region 1 rows: A = Si[x]
-// in all four bytes, addressed through lo.byte2 = 1 (region1()).
+// TL5 has LE bytes (14s, 9s, 13s, 11s); TL6/TL7/TL8 = rotl8/16/24 of it.
+// Column j takes b0(u_j), b1(u_j-1), b2(u_j-2), b3(u_j-3) (inverse
+// ShiftRows, cyr_rijndael.cpp:731-746).
+// 160 KiB decrypt image: region 0 = TL5 | TL6, region 1 = TL7 | TL8 (TL6/TL8
+// = rotl8 of TL5/TL7, made during the fill), so a middle-round column needs
+// no rotation (as ecol; A/B vs the 128 KiB TL5|TL7 image with one rotation
+// per column: same LDS cycles, -1.2 % time from the higher clock), and Si at
+// 128 KiB in 128-B rows (32 slots), addressed as (perm(u, lo, sel) >> 1):
+// lo = [lane*4, lane*8, 1, 4] gives x << 8 | lane*8 | 4 << 16 before the shift.
+__device__ __forceinline__ uint32_t dec_lo(uint32_t tid) {
+    return ((tid & 31u) << 2) | ((tid & 31u) << 11) | 0x10000u | 0x04000000u;
+}
+__device__ __forceinline__ uint32_t dcol(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
+                                         uint32_t x3, uint32_t k) {
+    const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));                   // TL5[b0]
+    const uint32_t l1 = ld(lds + kHalfB, addr(x1, lo, kSel1));          // TL6[b1]
+    const uint32_t l2 = ld(lds, addr(x2, lo, region1(kSel2)));          // TL7[b2]
+    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, region1(kSel3))); // TL8[b3]
+    return xor3(l0, l1, xor3(l2, l3, k));
+}
 __device__ __forceinline__ uint32_t dec_last(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
                                              uint32_t x3) {
-    const uint32_t l0 = ld(lds, addr(x0, lo, region1(kSel0)));
-    const uint32_t l1 = ld(lds, addr(x1, lo, region1(kSel1)));
-    const uint32_t l2 = ld(lds, addr(x2, lo, region1(kSel2)));
-    const uint32_t l3 = ld(lds, addr(x3, lo, region1(kSel3)));
+    const uint32_t l0 = ld(lds, addr(x0, lo, 0x0C030401u) >> 1);
+    const uint32_t l1 = ld(lds, addr(x1, lo, 0x0C030501u) >> 1);
+    const uint32_t l2 = ld(lds, addr(x2, lo, 0x0C030601u) >> 1);
+    const uint32_t l3 = ld(lds, addr(x3, lo, 0x0C030701u) >> 1);
     return merge4(l0, l1, l2, l3);
 }
+__device__ __forceinline__ void fill_dec_image(uint32_t* lds, const uint32_t* __restrict__ t) {
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+    for (int q = threadIdx.x; q < 8192; q += kDecThreads) {  // two 64 KiB T regions
+        const int region = q >> 12, half = (q >> 3) & 1, row = (q >> 4) & 255;
+        uint32_t v = t[256 * region + row];
+        if (half) v = rotl8(v);
+        l4[q] = make_uint4(v, v, v, v);
+    }
+    for (int q = threadIdx.x; q < 2048; q += kDecThreads) {  // Si: 256 rows x 128 B
+        const uint32_t v = t[512 + (q >> 3)];
+        l4[8192 + q] = make_uint4(v, v, v, v);
+    }
+}
+// prio_feedback counters of the decrypt workgroups: the 160 KiB image leaves
+// no LDS word free, so they live in global memory (one per workgroup, reset by
+// it at start; a collision between concurrent launches only blurs priorities).
+constexpr uint32_t kLeadSlots = 4096;
+__device__ unsigned int g_dec_lead[kLeadSlots];
 
 // Decrypts N independent blocks together (N-way ILP per LDS round trip) and
 // returns D(c[n]) ^ prev[n] in prev[n] (CBC, cyr_rijndael.cpp:625-630).
@@ -665,10 +686,9 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     constexpr int R = kDecRows;
     static_assert(R % 2 == 0, "rows are decrypted in pairs");
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
-    fill_region(lds_words, a.tables, a.tables + 256, kDecThreads);
-    fill_region(lds_words + 16384, a.tables + 512, nullptr, kDecThreads);
-    __shared__ uint32_t lead;  // prio_feedback
-    if (threadIdx.x == 0) lead = 0;
+    fill_dec_image(lds_words, a.tables);
+    unsigned int* leadp = &g_dec_lead[blockIdx.x % kLeadSlots];
+    if (threadIdx.x == 0) *leadp = 0;
     uint32_t prog = 0;
     __syncthreads();
     CLOCK_PROBE(1);
@@ -678,7 +698,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     if (begin >= a.nblocks) return;
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
+    const uint32_t lo = dec_lo(threadIdx.x);
     const uint64_t end = min(begin + a.blocks_per_wave, a.nblocks);
     FlatPos ps;
     ps.bp = begin / a.bpp.d;
@@ -705,7 +725,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
             for (int k = 0; k < R; k++) { c[k] = cn[k]; pv[k] = pvn[k]; }
         }
 #endif
-        prio_feedback(&lead, ++prog, kDecPrioDiv);
+        prio_feedback(leadp, ++prog, kDecPrioDiv);
         ps.bpos += a.step_r;
         ps.bp += a.step_q;
         if (ps.bpos >= a.bpp.d) { ps.bpos -= a.bpp.d; ps.bp++; }
@@ -720,15 +740,14 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
 __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     constexpr int R = kDecRows;
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
-    fill_region(lds_words, a.tables, a.tables + 256, kDecThreads);
-    fill_region(lds_words + 16384, a.tables + 512, nullptr, kDecThreads);
-    __shared__ uint32_t lead;  // prio_feedback
-    if (threadIdx.x == 0) lead = 0;
+    fill_dec_image(lds_words, a.tables);
+    unsigned int* leadp = &g_dec_lead[blockIdx.x % kLeadSlots];
+    if (threadIdx.x == 0) *leadp = 0;
     uint32_t prog = 0;
     __syncthreads();
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
+    const uint32_t lo = dec_lo(threadIdx.x);
     const uint64_t nwaves = (uint64_t)gridDim.x * (kDecThreads / 64);
     const uint64_t wave0 =
         (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -747,7 +766,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         uint4 carry = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
         if (nb == 0 && a.iv_out && lane == 0) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = carry;  // chain unchanged
         for (uint32_t base = 0; base < nb; base += 64 * R) {
-            prio_feedback(&lead, ++prog, kDecPrioDiv);
+            prio_feedback(leadp, ++prog, kDecPrioDiv);
             uint4 c[R], pv[R];
 #pragma unroll
             for (int k = 0; k < R; k++) {
@@ -816,7 +835,7 @@ __global__ void k_key_expand(const uint8_t* keys, uint32_t nkeys, const uint8_t*
         }
         w[j] = w[j - 4] ^ t;
     }
-    // Device layout (cyaes_internal.h): LE words, dk rounds 1..9 rotated right by 8.
+    // Device layout (cyaes_internal.h): LE words.
     uint32_t* s = sched + (uint64_t)i * kSchedWords;
     for (int j = 0; j < 44; j++) s[j] = __builtin_bswap32(w[j]);
     for (int r = 0; r <= 10; r++) {
@@ -829,8 +848,7 @@ __global__ void k_key_expand(const uint8_t* keys, uint32_t nkeys, const uint8_t*
                     ((gm(b0, 13) ^ gm(b1, 9) ^ gm(b2, 14) ^ gm(b3, 11)) << 8) |
                     (gm(b0, 11) ^ gm(b1, 13) ^ gm(b2, 9) ^ gm(b3, 14));
             }
-            const uint32_t v = __builtin_bswap32(t);
-            s[44 + 4 * r + c] = (r >= 1 && r <= 9) ? __builtin_rotateright32(v, 8) : v;
+            s[44 + 4 * r + c] = __builtin_bswap32(t);
         }
     }
 }

@@ -108,16 +108,11 @@ void expand_key(const uint8_t key[16], cyaes_key* out) {
         }
 }
 
-// Decryption middle rounds are stored rotr8 so the decrypt kernels can fold
-// the key into the rotated half of a column (cyaes_kernels.hip, dcol()).
-static bool rotated(int r) { return r > 0 && r < CYAES_ROUNDS; }
-
 void to_device_schedule(const cyaes_key& k, uint32_t out[88]) {
     for (int r = 0; r <= CYAES_ROUNDS; r++)
         for (int c = 0; c < 4; c++) {
             out[4 * r + c] = bswap(k.ke[r][c]);
-            const uint32_t d = bswap(k.kd[r][c]);
-            out[44 + 4 * r + c] = rotated(r) ? rotl(d, 24) : d;
+            out[44 + 4 * r + c] = bswap(k.kd[r][c]);
         }
 }
 
@@ -125,8 +120,7 @@ void from_device_schedule(const uint32_t in[88], cyaes_key* k) {
     for (int r = 0; r <= CYAES_ROUNDS; r++)
         for (int c = 0; c < 4; c++) {
             k->ke[r][c] = bswap(in[4 * r + c]);
-            const uint32_t d = in[44 + 4 * r + c];
-            k->kd[r][c] = bswap(rotated(r) ? rotl(d, 8) : d);
+            k->kd[r][c] = bswap(in[44 + 4 * r + c]);
         }
 }
 

@@ -24,7 +24,7 @@ const HostTables& host_tables();
 // Reference-layout schedule (Rijndael::Rijndael, cyr_rijndael.cpp:507-572).
 void expand_key(const uint8_t key[16], cyaes_key* out);
 
-// Device schedule: 88 little-endian words (ek[44], dk[44]); dk rounds 1..9 rotr8.
+// Device schedule: 88 little-endian words (ek[44], dk[44]).
 void to_device_schedule(const cyaes_key& k, uint32_t out[88]);
 void from_device_schedule(const uint32_t in[88], cyaes_key* k);
 
