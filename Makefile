@@ -15,8 +15,9 @@ ORACLE   := oracle/liboracle.so
 CPPTEST  := $(BUILD)/test_rijndael
 
 KSRC     := cyclone_amd/csrc/cyaes_kernels.hip
-HSRC     := cyclone_amd/csrc/cyaes_runtime.cpp cyclone_amd/csrc/cyaes_tables.cpp cyclone_amd/csrc/cyr_rijndael.cpp
-HDRS     := include/cyaes.h include/cyclone_amd/cyr_rijndael.h cyclone_amd/csrc/cyaes_internal.h \
+HSRC     := cyclone_amd/csrc/cyaes_runtime.cpp cyclone_amd/csrc/cyaes_tables.cpp cyclone_amd/csrc/cyr_rijndael.cpp \
+            cyclone_amd/csrc/cyaes_relay.cpp cyclone_amd/csrc/cyaes_batcher.cpp
+HDRS     := include/cyaes.h include/cyaes_relay.h include/cyaes_batch.h include/cyclone_amd/cyr_rijndael.h cyclone_amd/csrc/cyaes_internal.h \
             cyclone_amd/csrc/cyaes_tables.h
 
 KOBJ     := $(BUILD)/cyaes_kernels.o

@@ -78,15 +78,46 @@ _SIGS = {
     "cyaes_gpu_fill_synthetic": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                                 ctypes.c_uint64, _vp]),
     "cyaes_gpu_digest": (ctypes.c_int, [_vp, ctypes.c_uint64, _u64p, _vp]),
+    "cyaes_gpu_update_keys": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32]),
+    "cyaes_gpu_cbc_encrypt_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
+    "cyaes_gpu_cbc_decrypt_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
+    # include/cyaes_relay.h
+    "cyaes_relay_round16": (ctypes.c_uint32, [ctypes.c_uint32]),
+    "cyaes_relay_packet_bytes": (ctypes.c_uint32, [ctypes.c_uint32]),
+    "cyaes_relay_build_forward": (ctypes.c_uint32, [_vp, ctypes.c_int32, _vp, ctypes.c_uint32]),
+    "cyaes_relay_parse": (ctypes.c_uint32, [_vp, ctypes.c_size_t, _vp, _vp, _vp, ctypes.c_uint32,
+                                            ctypes.POINTER(ctypes.c_size_t)]),
+    "cyaes_relay_payloads": (ctypes.c_int64, [_vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint64, _vp, _vp]),
+    "cyaes_relay_forward_id": (ctypes.c_int32, [_vp]),
+    "cyaes_relay_forward_size": (ctypes.c_int32, [_vp]),
+    # include/cyaes_batch.h
+    "cyaes_batcher_create": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    "cyaes_batcher_destroy": (None, [_vp]),
+    "cyaes_batcher_session_open": (ctypes.c_int, [_vp, _vp, _u32p]),
+    "cyaes_batcher_session_close": (ctypes.c_int, [_vp, ctypes.c_uint32]),
+    "cyaes_batcher_submit": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32, _vp, _vp, ctypes.c_size_t, _vp,
+                                            _vp]),
+    "cyaes_batcher_submit_seal": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_int32, _vp, ctypes.c_uint32, _vp,
+                                                 _vp, _vp]),
+    "cyaes_batcher_submit_open": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp]),
+    "cyaes_batcher_flush": (ctypes.c_int, [_vp]),
+    "cyaes_batcher_stats": (ctypes.c_int, [_vp, _u64p]),
 }
 
 _lib = None
 
 
-def header_functions(path=HEADER_PATH):
-    """Names of the functions include/cyaes.h declares."""
-    text = open(path).read()
-    return sorted(set(re.findall(r"\b(cyaes_[a-z0-9_]+)\s*\(", text)))
+HEADERS = [os.path.join(os.path.dirname(_HERE), "include", h)
+           for h in ("cyaes.h", "cyaes_relay.h", "cyaes_batch.h")]
+
+
+def header_functions(paths=None):
+    """Names of the functions the C-ABI headers (include/cyaes*.h) declare."""
+    names = set()
+    for path in paths or HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(path).read(), flags=re.S)  # drop comments
+        names |= set(re.findall(r"\b(cyaes_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 def load_library(path=LIB_PATH):
@@ -140,8 +171,12 @@ class _Buf:
                 raise TypeError("output buffer is read-only")
             self.obj = obj
             self.n = mv.nbytes
-            self.arr = (ctypes.c_uint8 * max(self.n, 1)).from_buffer(mv) if not mv.readonly else \
-                (ctypes.c_uint8 * max(self.n, 1)).from_buffer_copy(mv.tobytes() or b"\0")
+            if self.n == 0:
+                self.arr = (ctypes.c_uint8 * 1)()  # never dereferenced for size 0
+            elif mv.readonly:
+                self.arr = (ctypes.c_uint8 * self.n).from_buffer_copy(mv.tobytes())
+            else:
+                self.arr = (ctypes.c_uint8 * self.n).from_buffer(mv)
         else:
             if writable:
                 raise TypeError("output must be a writable buffer (bytearray)")
@@ -292,3 +327,162 @@ class GpuContext:
         out = (ctypes.c_uint64 * 2)()
         _check(self._lib.cyaes_gpu_digest(_p(d_buf), nbytes, out, _p(stream)), "digest")
         return int(out[0]), int(out[1])
+
+
+# ---- relay wire format (include/cyaes_relay.h) ------------------------------
+RELAY_HEADSIZE, RELAY_FORWARD, RELAY_PAYLOAD_OFFSET, RELAY_MAX_CHUNK, RELAY_PAD = 4, 103, 12, 0xFF00, 0xCE
+
+
+def relay_packet_bytes(msg_size):
+    return load_library().cyaes_relay_packet_bytes(msg_size)
+
+
+def relay_build_forward(conn_id, payload):
+    """Plaintext RELAY_FORWARD packet (relay_local.cpp:189-201) as bytes."""
+    payload = bytes(payload)
+    lib = load_library()
+    out = (ctypes.c_uint8 * lib.cyaes_relay_packet_bytes(len(payload)))()
+    src = (ctypes.c_uint8 * max(1, len(payload))).from_buffer_copy(payload or b"\0")
+    n = lib.cyaes_relay_build_forward(out, conn_id, src if payload else None, len(payload))
+    if n == 0:
+        raise ValueError("chunk larger than RELAY_MAX_CHUNK")
+    return bytes(out)[:n]
+
+
+def relay_parse(stream, max_packets=1 << 20):
+    """[(offset, packet_size, packet_id)], consumed bytes (cye_packet.cpp:166-181)."""
+    stream = bytes(stream)
+    lib = load_library()
+    cap = min(max_packets, len(stream) // RELAY_HEADSIZE + 1)
+    off = (ctypes.c_uint64 * cap)()
+    sz = (ctypes.c_uint32 * cap)()
+    ids = (ctypes.c_uint16 * cap)()
+    used = ctypes.c_size_t()
+    buf = (ctypes.c_uint8 * max(1, len(stream))).from_buffer_copy(stream or b"\0")
+    n = lib.cyaes_relay_parse(buf, len(stream), off, sz, ids, cap, ctypes.byref(used))
+    return [(off[i], sz[i], ids[i]) for i in range(n)], used.value
+
+
+def relay_payloads(packets, base=0):
+    """(payload offsets, payload sizes) of the RELAY_FORWARD packets of a parsed stream."""
+    lib = load_library()
+    n = len(packets)
+    off = (ctypes.c_uint64 * max(1, n))(*[p[0] for p in packets])
+    sz = (ctypes.c_uint32 * max(1, n))(*[p[1] for p in packets])
+    ids = (ctypes.c_uint16 * max(1, n))(*[p[2] for p in packets])
+    po = (ctypes.c_uint64 * max(1, n))()
+    pl = (ctypes.c_uint32 * max(1, n))()
+    j = lib.cyaes_relay_payloads(off, sz, ids, n, base, po, pl)
+    if j < 0:
+        raise ValueError("RELAY_FORWARD packet with a payload that is not a multiple of 16")
+    return list(po[:j]), list(pl[:j])
+
+
+# ---- asynchronous batching adapter (include/cyaes_batch.h) ------------------
+OP_ENCRYPT, OP_DECRYPT, OP_RELAY_SEAL, OP_RELAY_OPEN = 0, 1, 2, 3
+_DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)
+
+
+class BatcherConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("max_batch_bytes", ctypes.c_uint32),
+                ("max_delay_us", ctypes.c_uint32), ("inflight", ctypes.c_uint32)]
+
+
+class Batcher:
+    """cyaes_batcher: requests from any thread are coalesced into GPU batches.
+
+    Buffers are host buffers (bytearray / writable memoryview); they are kept
+    alive by the batcher until the request completes.  `done(status)` runs on
+    the batcher's completion thread."""
+
+    def __init__(self, device=0, max_batch_bytes=0, max_delay_us=0, inflight=0, lib=None):
+        self._lib = lib if lib is not None else load_library()
+        cfg = BatcherConfig(device, max_batch_bytes, max_delay_us, inflight)
+        h = _vp()
+        _check(self._lib.cyaes_batcher_create(ctypes.byref(cfg), ctypes.byref(h)), "cyaes_batcher_create")
+        self._h = h
+        self._live = {}
+        self._next = 1
+        self._mu = __import__("threading").Lock()
+        self._cb = _DONE_FN(self._on_done)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.cyaes_batcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _on_done(self, user, status):
+        with self._mu:
+            bufs, done = self._live.pop(user)
+        if done is not None:
+            done(status)
+
+    def _track(self, bufs, done):
+        with self._mu:
+            token = self._next
+            self._next += 1
+            self._live[token] = (bufs, done)
+        return token
+
+    def _untrack(self, token):
+        with self._mu:
+            self._live.pop(token, None)
+
+    def session_open(self, key):
+        key = bytes(key)
+        if len(key) != 16:
+            raise ValueError("AES-128 key must be 16 bytes")
+        slot = ctypes.c_uint32()
+        _check(self._lib.cyaes_batcher_session_open(self._h, (ctypes.c_uint8 * 16).from_buffer_copy(key),
+                                                    ctypes.byref(slot)), "session_open")
+        return slot.value
+
+    def session_close(self, slot):
+        _check(self._lib.cyaes_batcher_session_close(self._h, slot), "session_close")
+
+    def submit(self, op, slot, inp, out, size=None, done=None):
+        src = _Buf(inp, False)
+        dst = src if out is inp else _Buf(out, True)
+        size = src.n if size is None else size
+        if size > src.n or size > dst.n:
+            raise ValueError("size exceeds buffer")
+        token = self._track((src, dst), done)
+        st = self._lib.cyaes_batcher_submit(self._h, op, slot, src.ptr, dst.ptr, size, self._cb, token)
+        if st:
+            self._untrack(token)
+            raise CyaesError(st, "submit")
+
+    def submit_seal(self, slot, conn_id, payload, packet_out, done=None):
+        src = _Buf(payload, False)
+        dst = _Buf(packet_out, True)
+        if dst.n < relay_packet_bytes(src.n):
+            raise ValueError("packet_out too small")
+        token = self._track((src, dst), done)
+        st = self._lib.cyaes_batcher_submit_seal(self._h, slot, conn_id, src.ptr, src.n, dst.ptr, self._cb, token)
+        if st:
+            self._untrack(token)
+            raise CyaesError(st, "submit_seal")
+
+    def submit_open(self, slot, packet, done=None):
+        buf = _Buf(packet, True)
+        token = self._track((buf,), done)
+        st = self._lib.cyaes_batcher_submit_open(self._h, slot, buf.ptr, buf.n, self._cb, token)
+        if st:
+            self._untrack(token)
+            raise CyaesError(st, "submit_open")
+
+    def flush(self):
+        """Waits for every request submitted so far; returns the first error status (0 = none)."""
+        return self._lib.cyaes_batcher_flush(self._h)
+
+    def stats(self):
+        out = (ctypes.c_uint64 * 6)()
+        _check(self._lib.cyaes_batcher_stats(self._h, out), "stats")
+        keys = ("completed", "batches", "bytes", "max_batch", "errors", "pending")
+        return dict(zip(keys, (int(v) for v in out)))

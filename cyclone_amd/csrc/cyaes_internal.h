@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+struct cyaes_gpu;  // include/cyaes.h
+
 namespace cyaes {
 
 // Device key schedule: the reference's m_Ke / m_Kd words (cyr_rijndael.h:50,52)
@@ -101,5 +103,12 @@ hipError_t launch_key_expand(const uint8_t* d_keys, uint32_t nkeys, const uint8_
 hipError_t launch_fill_synthetic(uint8_t* buf, uint64_t p0, uint64_t npayloads, uint32_t payload_bytes,
                                  uint64_t seed, hipStream_t stream);
 hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long* out2, hipStream_t stream);
+
+// Host runtime (cyaes_runtime.cpp): ragged batch under an explicit device key
+// table of table_keys schedules (the batcher's per-batch session keys).
+// key_idx (device, nullable => key 0) indexes that table.
+int ragged_batch(cyaes_gpu* ctx, bool decrypt, const uint32_t* d_table, uint32_t table_keys, const uint8_t* in,
+                 uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes, uint64_t npayloads,
+                 const uint32_t* key_idx, hipStream_t stream);
 
 }  // namespace cyaes

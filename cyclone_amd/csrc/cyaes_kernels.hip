@@ -304,6 +304,28 @@ constexpr uint32_t kEncPrioDiv = 4;  // steps = 8-block chunks (A/B: 1, 2, 4, 8 
 constexpr uint32_t kDecPrioDiv = 8;  // steps = 64*kDecRows-block rows (A/B: 4, 8, 16 -> 8)
 
 
+// 16-B block at a 4-byte-aligned address (ragged batches: relay packets put
+// the payload at packet offset 12).  Still one global_load/store_dwordx4.
+struct __attribute__((aligned(4))) Blk4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ uint4 ldu(const uint8_t* p) {
+    const Blk4 v = *reinterpret_cast<const Blk4*>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void stu(uint8_t* p, uint4 v) { *reinterpret_cast<Blk4*>(p) = Blk4{v.x, v.y, v.z, v.w}; }
+// Block i of a payload: 16-B aligned (U = false) or 4-B aligned (U = true).
+template <bool U>
+__device__ __forceinline__ uint4 ldb(const uint8_t* base, uint32_t i) {
+    if (U) return ldu(base + 16ull * i);
+    return reinterpret_cast<const uint4*>(base)[i];
+}
+template <bool U>
+__device__ __forceinline__ void stb(uint8_t* base, uint32_t i, uint4 v) {
+    if (U) stu(base + 16ull * i, v);
+    else reinterpret_cast<uint4*>(base)[i] = v;
+}
+
 __device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kIv2, kIv3); }
 
 #if CYAES_CLOCK_PROBE
@@ -375,13 +397,13 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                 uint32_t ek[44];
                 load_sched(a.keys.table + (uint64_t)ku * kSchedWords, ek);
                 uint4 c = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
-                const uint4* src = reinterpret_cast<const uint4*>(a.in + off);
-                uint4* dst = reinterpret_cast<uint4*>(a.out + off);
+                const uint8_t* src = a.in + off;  // ragged: 4-B aligned
+                uint8_t* dst = a.out + off;
                 uint32_t i = 0;
                 uint4 b[8];
                 if (nb >= 8) {
 #pragma unroll
-                    for (int j = 0; j < 8; j++) b[j] = src[j];
+                    for (int j = 0; j < 8; j++) b[j] = ldb<RAGGED>(src, j);
                 }
                 for (; i + 8 <= nb; i += 8) {
 #if !CYAES_NO_PREFETCH  // A/B: -8% encrypt time vs loading at the top of the chunk
@@ -389,7 +411,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                     const bool more = i + 16 <= nb;
                     if (more) {
 #pragma unroll
-                        for (int j = 0; j < 8; j++) bn[j] = src[i + 8 + j];
+                        for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(src, i + 8 + j);
                     }
 #endif
                     prio_feedback(&lead, ++prog, kEncPrioDiv);
@@ -402,11 +424,11 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                         b[j] = c;
                     }
 #pragma unroll
-                    for (int j = 0; j < 8; j++) dst[i + j] = b[j];  // (nt stores measured 3.6x slower)
+                    for (int j = 0; j < 8; j++) stb<RAGGED>(dst, i + j, b[j]);  // (nt stores measured 3.6x slower)
 #if CYAES_NO_PREFETCH
                     if (i + 16 <= nb) {
 #pragma unroll
-                        for (int j = 0; j < 8; j++) b[j] = src[i + 8 + j];
+                        for (int j = 0; j < 8; j++) b[j] = ldb<RAGGED>(src, i + 8 + j);
                     }
 #else
                     if (more) {
@@ -416,12 +438,12 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
 #endif
                 }
                 for (; i < nb; i++) {
-                    const uint4 v = src[i];
+                    const uint4 v = ldb<RAGGED>(src, i);
                     uint32_t s0 = xor3(c.x, v.x, ek[0]), s1 = xor3(c.y, v.y, ek[1]);
                     uint32_t s2 = xor3(c.z, v.z, ek[2]), s3 = xor3(c.w, v.w, ek[3]);
                     enc_block(lds, lo, ek, s0, s1, s2, s3);
                     c = make_uint4(s0, s1, s2, s3);
-                    dst[i] = c;
+                    stb<RAGGED>(dst, i, c);
                 }
                 if (a.iv_out) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c;
             }
@@ -752,8 +774,8 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     const uint64_t wave0 =
         (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (uint64_t p = wave0; p < a.npayloads; p += nwaves) {
-        const uint4* in = reinterpret_cast<const uint4*>(a.in + a.offsets[p]);
-        uint4* out = reinterpret_cast<uint4*>(a.out + a.offsets[p]);
+        const uint8_t* in = a.in + a.offsets[p];  // 4-B aligned
+        uint8_t* out = a.out + a.offsets[p];
         const uint32_t nb = a.nbytes[p] >> 4;
         uint32_t kid = a.keys.key_idx ? a.keys.key_idx[p] : (a.keys.ppk.d ? fastdiv((uint32_t)p, a.keys.ppk) : 0u);
         if (kid >= a.keys.nkeys) {
@@ -771,7 +793,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 const uint32_t g = base + 64 * k + lane;
-                c[k] = g < nb ? in[g] : make_uint4(0, 0, 0, 0);
+                c[k] = g < nb ? ldu(in + 16ull * g) : make_uint4(0, 0, 0, 0);
             }
             // predecessors from the neighbour lane (as k_decrypt_flat): no loads of
             // other lanes' blocks, so in-place needs no drain
@@ -788,7 +810,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 const uint32_t g = base + 64 * k + lane;
-                if (g < nb) out[g] = pv[k];
+                if (g < nb) stu(out + 16ull * g, pv[k]);
             }
             carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
         }

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <vector>
 
 #include "cyaes.h"
 #include "cyaes_internal.h"
@@ -71,15 +72,19 @@ int ensure(T** buf, uint64_t* cap, uint64_t want_elems) {
     return CYAES_OK;
 }
 
-// Validates the key-selection arguments of a batch and fills a KeySel.
-int make_keysel(const cyaes_gpu* ctx, uint64_t npayloads, const uint32_t* key_idx, uint32_t ppk, KeySel* ks) {
-    if (ctx->nkeys == 0) return CYAES_ERANGE;
+// Validates the key-selection arguments of a batch and fills a KeySel.  The
+// key table is the context's, unless a batch brings its own (table != NULL:
+// the drop-in's per-call schedule, the batcher's per-batch session keys).
+int make_keysel(const cyaes_gpu* ctx, uint64_t npayloads, const uint32_t* key_idx, uint32_t ppk, KeySel* ks,
+                const uint32_t* table = nullptr, uint32_t table_keys = 0) {
+    const uint32_t nkeys = table ? table_keys : ctx->nkeys;
+    if (nkeys == 0) return CYAES_ERANGE;
     if ((key_idx || ppk) && npayloads > 0xFFFFFFFFull) return CYAES_EINVAL;
-    if (!key_idx && ppk && npayloads && (npayloads - 1) / ppk >= ctx->nkeys) return CYAES_ERANGE;
-    ks->table = ctx->d_keys;
+    if (!key_idx && ppk && npayloads && (npayloads - 1) / ppk >= nkeys) return CYAES_ERANGE;
+    ks->table = table ? table : ctx->d_keys;
     ks->key_idx = key_idx;
     ks->ppk = key_idx ? make_fastdiv(0) : make_fastdiv(ppk);
-    ks->nkeys = ctx->nkeys;
+    ks->nkeys = nkeys;
     return CYAES_OK;
 }
 
@@ -88,9 +93,10 @@ int dec_grid_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kDecW
 
 int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
                    uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk,
-                   const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream) {
+                   const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream, const uint32_t* table = nullptr,
+                   uint32_t table_keys = 0) {
     EncArgs a = {};
-    int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys);
+    int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys, table, table_keys);
     if (st) return st;
     a.in = in;
     a.out = out;
@@ -120,9 +126,10 @@ int alias_iv(cyaes_gpu* ctx, const uint8_t** iv_in, const uint8_t* iv_out, uint6
 }
 
 int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t npayloads, uint32_t payload_bytes,
-                    const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream) {
+                    const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream,
+                    const uint32_t* table = nullptr, uint32_t table_keys = 0) {
     DecArgs a = {};
-    int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys);
+    int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys, table, table_keys);
     if (st) return st;
     if ((iv_in || iv_out) && npayloads > 0xFFFFFFFFull) return CYAES_EINVAL;
     const uint32_t bpp = payload_bytes / 16;
@@ -161,9 +168,9 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
 
 int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
                    uint64_t npayloads, const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in, uint8_t* iv_out,
-                   hipStream_t stream) {
+                   hipStream_t stream, const uint32_t* table = nullptr, uint32_t table_keys = 0) {
     DecArgs a = {};
-    int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys);
+    int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys, table, table_keys);
     if (st) return st;
     st = alias_iv(ctx, &iv_in, iv_out, npayloads, stream);
     if (st) return st;
@@ -183,12 +190,33 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     return map_err(launch_decrypt_ragged(a, grid, stream));
 }
 
+bool aligned4(const void* p) { return ((uintptr_t)p & 3u) == 0; }
+
 bool batch_args_ok(const cyaes_gpu* ctx, const uint8_t* in, const uint8_t* out, const void* iv_in,
                    const void* iv_out) {
     return ctx && in && out && aligned16(in) && aligned16(out) && aligned16(iv_in) && aligned16(iv_out);
 }
 
+// Ragged payloads may sit at any 4-byte-aligned offset (relay packets carry
+// the payload at packet offset 12, relay_protocol.h:5-7,36-42).
+bool ragged_args_ok(const cyaes_gpu* ctx, const uint8_t* in, const uint8_t* out, const void* iv_in,
+                    const void* iv_out) {
+    return ctx && in && out && aligned4(in) && aligned4(out) && aligned16(iv_in) && aligned16(iv_out);
+}
+
 }  // namespace
+
+int cyaes::ragged_batch(cyaes_gpu* ctx, bool decrypt, const uint32_t* d_table, uint32_t table_keys,
+                        const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
+                        uint64_t npayloads, const uint32_t* key_idx, hipStream_t stream) {
+    if (!ctx || !d_table || !offsets || !nbytes || !ragged_args_ok(ctx, in, out, nullptr, nullptr)) return CYAES_EINVAL;
+    if (npayloads == 0) return CYAES_OK;
+    DeviceGuard g(ctx->device);
+    return decrypt ? decrypt_ragged(ctx, in, out, offsets, nbytes, npayloads, key_idx, 0, nullptr, nullptr, stream,
+                                    d_table, table_keys)
+                   : encrypt_common(ctx, in, out, offsets, nbytes, npayloads, 0, key_idx, 0, nullptr, nullptr, stream,
+                                    d_table, table_keys);
+}
 
 extern "C" {
 
@@ -295,6 +323,37 @@ int cyaes_gpu_set_keys(cyaes_gpu* ctx, const uint8_t* keys, uint32_t nkeys) {
     return CYAES_OK;
 }
 
+int cyaes_gpu_update_keys(cyaes_gpu* ctx, uint32_t first, const uint8_t* keys, uint32_t n) {
+    if (!ctx || !keys || n == 0 || first > ctx->nkeys || (uint64_t)first + n > 0xFFFFFFFFull) return CYAES_EINVAL;
+    DeviceGuard g(ctx->device);
+    const uint32_t total = std::max(ctx->nkeys, first + n);
+    std::vector<uint32_t> host((size_t)n * kSchedWords);
+    for (uint32_t i = 0; i < n; i++) {
+        cyaes_key k;
+        expand_key(keys + 16ull * i, &k);
+        to_device_schedule(k, host.data() + (size_t)i * kSchedWords);
+    }
+    CY_TRY(hipDeviceSynchronize());  // no batch may still read the rows being replaced
+    if (total > ctx->key_cap) {      // grow, keeping rows [0, first)
+        const uint32_t cap = std::max(total, ctx->key_cap * 2);
+        uint32_t* grown = nullptr;
+        CY_TRY(hipMalloc(reinterpret_cast<void**>(&grown), (uint64_t)cap * kSchedWords * 4));
+        hipError_t e = hipSuccess;
+        if (first) e = hipMemcpy(grown, ctx->d_keys, (uint64_t)first * kSchedWords * 4, hipMemcpyDeviceToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(grown);
+            return map_err(e);
+        }
+        (void)hipFree(ctx->d_keys);
+        ctx->d_keys = grown;
+        ctx->key_cap = cap;
+    }
+    CY_TRY(hipMemcpy(ctx->d_keys + (uint64_t)first * kSchedWords, host.data(), host.size() * 4,
+                     hipMemcpyHostToDevice));
+    ctx->nkeys = total;
+    return CYAES_OK;
+}
+
 int cyaes_gpu_set_keys_device(cyaes_gpu* ctx, const uint8_t* d_keys, uint32_t nkeys, void* stream) {
     if (!ctx || !d_keys || nkeys == 0) return CYAES_EINVAL;
     DeviceGuard g(ctx->device);
@@ -359,7 +418,7 @@ int cyaes_gpu_encrypt_ragged(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out
                              uint32_t payloads_per_key, const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream) {
     if (!ctx) return CYAES_EINVAL;
     if (npayloads == 0) return CYAES_OK;
-    if (!d_offsets || !d_nbytes || !batch_args_ok(ctx, d_in, d_out, d_iv_in, d_iv_out)) return CYAES_EINVAL;
+    if (!d_offsets || !d_nbytes || !ragged_args_ok(ctx, d_in, d_out, d_iv_in, d_iv_out)) return CYAES_EINVAL;
     DeviceGuard g(ctx->device);
     return encrypt_common(ctx, d_in, d_out, d_offsets, d_nbytes, npayloads, 0, d_key_idx, payloads_per_key, d_iv_in,
                           d_iv_out, (hipStream_t)stream);
@@ -370,10 +429,24 @@ int cyaes_gpu_decrypt_ragged(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out
                              uint32_t payloads_per_key, const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream) {
     if (!ctx) return CYAES_EINVAL;
     if (npayloads == 0) return CYAES_OK;
-    if (!d_offsets || !d_nbytes || !batch_args_ok(ctx, d_in, d_out, d_iv_in, d_iv_out)) return CYAES_EINVAL;
+    if (!d_offsets || !d_nbytes || !ragged_args_ok(ctx, d_in, d_out, d_iv_in, d_iv_out)) return CYAES_EINVAL;
     DeviceGuard g(ctx->device);
     return decrypt_ragged(ctx, d_in, d_out, d_offsets, d_nbytes, npayloads, d_key_idx, payloads_per_key, d_iv_in,
                           d_iv_out, (hipStream_t)stream);
+}
+
+int cyaes_gpu_cbc_encrypt_batch(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, const uint64_t* d_offsets,
+                                const uint32_t* d_nbytes, const uint32_t* d_key_idx, const uint8_t* d_iv,
+                                uint32_t npayloads, void* stream) {
+    return cyaes_gpu_encrypt_ragged(ctx, d_in, d_out, d_offsets, d_nbytes, npayloads, d_key_idx, 0, d_iv, nullptr,
+                                    stream);
+}
+
+int cyaes_gpu_cbc_decrypt_batch(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, const uint64_t* d_offsets,
+                                const uint32_t* d_nbytes, const uint32_t* d_key_idx, const uint8_t* d_iv,
+                                uint32_t npayloads, void* stream) {
+    return cyaes_gpu_decrypt_ragged(ctx, d_in, d_out, d_offsets, d_nbytes, npayloads, d_key_idx, 0, d_iv, nullptr,
+                                    stream);
 }
 
 int cyaes_gpu_check(cyaes_gpu* ctx) {
@@ -441,8 +514,7 @@ int dropin_ready(DropIn& d, uint64_t size) {
         if (st) return st;
         DeviceGuard g(d.ctx->device);
         CY_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-        // One key slot: the schedule travels with each call's staging copy.
-        d.ctx->nkeys = 1;
+        // The schedule travels with each call's staging copy (no context key table).
     }
     DeviceGuard g(d.ctx->device);
     const uint64_t need_host = 368 + size;
@@ -483,14 +555,13 @@ int dropin_run(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* o
     const uint64_t image = 368 + size;
     CY_TRY(hipMemcpyAsync(d.d_buf, d.pinned, image, hipMemcpyHostToDevice, d.stream));
     cyaes_gpu* ctx = d.ctx;
-    ctx->d_keys = reinterpret_cast<uint32_t*>(d.d_buf);
+    const uint32_t* d_sched = reinterpret_cast<const uint32_t*>(d.d_buf);
     const uint8_t* d_iv = d.d_buf + 352;
     const uint8_t* d_in = d.d_buf + 368;
     uint8_t* d_out = d.d_buf + image;
-    st = decrypt ? decrypt_uniform(ctx, d_in, d_out, 1, (uint32_t)size, nullptr, 0, d_iv, nullptr, d.stream)
+    st = decrypt ? decrypt_uniform(ctx, d_in, d_out, 1, (uint32_t)size, nullptr, 0, d_iv, nullptr, d.stream, d_sched, 1)
                  : encrypt_common(ctx, d_in, d_out, nullptr, nullptr, 1, (uint32_t)size, nullptr, 0, d_iv, nullptr,
-                                  d.stream);
-    ctx->d_keys = nullptr;
+                                  d.stream, d_sched, 1);
     if (st) return st;
     CY_TRY(hipMemcpyAsync(d.pinned, d_out, size, hipMemcpyDeviceToHost, d.stream));
     CY_TRY(hipStreamSynchronize(d.stream));

@@ -84,6 +84,12 @@ int cyaes_gpu_num_cus(const cyaes_gpu* ctx);
  * `stream` (set_keys is fully synchronous). */
 int cyaes_gpu_set_keys(cyaes_gpu* ctx, const uint8_t* keys, uint32_t nkeys);
 int cyaes_gpu_set_keys_device(cyaes_gpu* ctx, const uint8_t* d_keys, uint32_t nkeys, void* stream);
+/* Replaces (or appends) schedules [first, first + n) from n raw keys, growing
+ * the table if needed; rows outside the range are kept.  first <= nkeys.
+ * Per-session key plumbing: a relay session opens (relay_server.cpp:218-240,
+ * a new Rijndael pair per DH handshake) or its slot is reused after a close
+ * (relay_server.cpp:370-375).  Synchronous, like set_keys. */
+int cyaes_gpu_update_keys(cyaes_gpu* ctx, uint32_t first, const uint8_t* keys, uint32_t n);
 uint32_t cyaes_gpu_nkeys(const cyaes_gpu* ctx);
 /* Copies schedule `index` back in reference layout (m_Ke/m_Kd). Synchronous. */
 int cyaes_gpu_get_key(cyaes_gpu* ctx, uint32_t index, cyaes_key* out);
@@ -99,7 +105,9 @@ int cyaes_gpu_get_key(cyaes_gpu* ctx, uint32_t index, cyaes_key* out);
  *
  * Uniform layout: payload p occupies bytes [p*payload_bytes, (p+1)*payload_bytes).
  * Ragged layout:  payload p occupies [d_offsets[p], d_offsets[p] + d_nbytes[p]);
- *                 offsets and sizes must be multiples of 16. */
+ *                 sizes must be multiples of 16, offsets (and d_in/d_out)
+ *                 multiples of 4, so a relay packet's payload at packet
+ *                 offset 12 can be processed where it lies. */
 int cyaes_gpu_encrypt_uniform(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, uint64_t npayloads,
                               uint32_t payload_bytes, const uint32_t* d_key_idx, uint32_t payloads_per_key,
                               const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream);
@@ -112,6 +120,16 @@ int cyaes_gpu_encrypt_ragged(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out
 int cyaes_gpu_decrypt_ragged(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, const uint64_t* d_offsets,
                              const uint32_t* d_nbytes, uint64_t npayloads, const uint32_t* d_key_idx,
                              uint32_t payloads_per_key, const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream);
+
+/* The batch entry points of SURVEY.md §8(b), as ragged batches with one
+ * input IV per payload (d_iv: 16 B per payload, NULL => DefaultIV), key
+ * d_key_idx[p] (NULL => key 0) and no IV write-back. */
+int cyaes_gpu_cbc_encrypt_batch(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, const uint64_t* d_offsets,
+                                const uint32_t* d_nbytes, const uint32_t* d_key_idx, const uint8_t* d_iv,
+                                uint32_t npayloads, void* stream);
+int cyaes_gpu_cbc_decrypt_batch(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, const uint64_t* d_offsets,
+                                const uint32_t* d_nbytes, const uint32_t* d_key_idx, const uint8_t* d_iv,
+                                uint32_t npayloads, void* stream);
 
 /* Synchronises the context's last-used stream and returns CYAES_ERANGE if a
  * batch since the previous check saw an out-of-range key index (sticky flag

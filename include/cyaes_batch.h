@@ -1,0 +1,97 @@
+/*
+ * cyaes_batch.h -- asynchronous batching adapter.
+ *
+ * The reference calls Rijndael::encrypt/decrypt synchronously, one relay
+ * packet at a time, on each pipe's looper thread (relay_local.cpp:188-217,
+ * 365; relay_server.cpp:329, 453-481).  A single packet is one CBC chain of
+ * at most 4,080 blocks, so on a GPU it is all latency.  This adapter takes
+ * those calls from any number of threads, coalesces whatever arrives within
+ * a short window into one pinned staging buffer (gather), runs one ragged
+ * batch on the MI355X, copies the results back to the callers' buffers
+ * (scatter) and invokes each request's completion callback -- where a relay
+ * would then post TcpConnection::send to its looper.
+ *
+ * Sessions (row 3): every request names a session slot.  A slot holds the
+ * key of one relay pipe direction (relay_server.cpp:218-240 creates the
+ * Rijndael pair after the DH handshake; :370-375 deletes it on close).
+ * Schedules are expanded once on open (host) and travel with each batch that
+ * uses them, so opening/closing sessions never races in-flight batches.
+ *
+ * Request semantics = Rijndael::encrypt / decrypt (cyr_rijndael.cpp:588-635)
+ * with iv == nullptr, as every relay call site passes: one CBC chain from
+ * DefaultIV per request; size % 16 == 0; in == out allowed.
+ * RELAY_SEAL / RELAY_OPEN are the relay's packet operations (cyaes_relay.h):
+ *   SEAL: build the RELAY_FORWARD packet for a chunk (header, RelayForwardMsg,
+ *         0xCE padding) and encrypt its payload (relay_local.cpp:189-206);
+ *   OPEN: decrypt a received RELAY_FORWARD packet's payload in place
+ *         (relay_server.cpp:329).
+ *
+ * Pipelining: `inflight` staging buffers; while the GPU runs batch k the
+ * builder thread gathers batch k+1 and the completion thread scatters k-1.
+ * Callbacks run on the completion thread, in batch order; they must not
+ * block on the batcher (flush/destroy) themselves.
+ */
+#ifndef CYAES_BATCH_H
+#define CYAES_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CYAES_OP_ENCRYPT 0
+#define CYAES_OP_DECRYPT 1
+#define CYAES_OP_RELAY_SEAL 2
+#define CYAES_OP_RELAY_OPEN 3
+
+typedef struct cyaes_batcher cyaes_batcher;
+
+/* Completion: status is CYAES_OK or a CYAES_E* code (cyaes.h). */
+typedef void (*cyaes_done_fn)(void* user, int status);
+
+typedef struct cyaes_batcher_config {
+    int device;               /* HIP device                                          */
+    uint32_t max_batch_bytes; /* staging bytes per batch (0 => 32 MiB); caps a request */
+    uint32_t max_delay_us;    /* longest a request waits for company (0 => 100 us)     */
+    uint32_t inflight;        /* staging buffers / batches in flight (0 => 3)          */
+} cyaes_batcher_config;
+
+int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out);
+/* Completes every submitted request, then frees everything. */
+void cyaes_batcher_destroy(cyaes_batcher* b);
+
+/* Session slots.  open returns the lowest free slot. close frees it; requests
+ * already submitted under it still complete with the old key. */
+int cyaes_batcher_session_open(cyaes_batcher* b, const uint8_t key[16], uint32_t* slot);
+int cyaes_batcher_session_close(cyaes_batcher* b, uint32_t slot);
+
+/* op ENCRYPT / DECRYPT: out[0, size) = CBC(in[0, size)) under the slot's key.
+ * CYAES_EINVAL: size % 16, size > max_batch_bytes, NULL buffer, bad op;
+ * CYAES_ERANGE: slot not open.  On an error return `done` is not called. */
+int cyaes_batcher_submit(cyaes_batcher* b, int op, uint32_t slot, const uint8_t* in, uint8_t* out, size_t size,
+                         cyaes_done_fn done, void* user);
+/* RELAY_SEAL: packet_out receives cyaes_relay_packet_bytes(size) bytes,
+ * size <= CYAES_RELAY_MAX_CHUNK. */
+int cyaes_batcher_submit_seal(cyaes_batcher* b, uint32_t slot, int32_t conn_id, const uint8_t* payload,
+                              uint32_t size, uint8_t* packet_out, cyaes_done_fn done, void* user);
+/* RELAY_OPEN: packet holds one complete RELAY_FORWARD packet of packet_bytes
+ * (= 4 + packet_size); its payload is decrypted in place. */
+int cyaes_batcher_submit_open(cyaes_batcher* b, uint32_t slot, uint8_t* packet, uint32_t packet_bytes,
+                              cyaes_done_fn done, void* user);
+
+/* Blocks until every request submitted before the call has completed
+ * (callbacks returned).  Returns the first error status seen since the
+ * previous flush, else CYAES_OK. */
+int cyaes_batcher_flush(cyaes_batcher* b);
+
+/* out[0..5] = requests completed, batches, payload bytes, largest batch
+ * (requests), requests completed with an error, requests pending. */
+int cyaes_batcher_stats(cyaes_batcher* b, uint64_t out[6]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CYAES_BATCH_H */

@@ -1,0 +1,222 @@
+"""Batching adapter (include/cyaes_batch.h) and
+device-resident relay streams (include/cyaes_relay.h, row 2) on the MI355X,
+checked against the AES oracle and the relay restatement
+(oracle/relay_oracle.py).  Each request must equal the reference's
+synchronous Rijndael call with iv = nullptr (relay_local.cpp:206,365;
+relay_server.cpp:329,472)."""
+import random
+import struct
+import threading
+
+import pytest
+
+import cyclone_amd as ca
+import oracle
+import relay_oracle as ro
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def batcher():
+    b = ca.Batcher(0, max_batch_bytes=4 << 20, max_delay_us=200)
+    yield b
+    b.close()
+
+
+def _keys(n, seed):
+    rng = random.Random(seed)
+    return [bytes(rng.randrange(256) for _ in range(16)) for _ in range(n)]
+
+
+def test_mixed_requests_from_threads_match_oracle(batcher):
+    keys = _keys(6, 1)
+    slots = [batcher.session_open(k) for k in keys]
+    results = []
+    lock = threading.Lock()
+
+    def worker(tid):
+        rng = random.Random(100 + tid)
+        for i in range(150):
+            op = rng.choice([ca.OP_ENCRYPT, ca.OP_DECRYPT])
+            k = rng.randrange(len(keys))
+            size = 16 * rng.choice([0, 1, 2, 63, 64, 92, 255, 256, 1000, rng.randrange(0, 4081)])
+            data = bytes(rng.randrange(256) for _ in range(size))
+            inplace = rng.random() < 0.3
+            out = bytearray(data) if inplace else bytearray(size)
+            inp = out if inplace else data
+            rec = {"op": op, "k": k, "data": data, "out": out, "status": None}
+
+            def done(status, rec=rec):
+                rec["status"] = status
+            batcher.submit(op, slots[k], inp, out, size, done)
+            with lock:
+                results.append(rec)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert batcher.flush() == ca.CYAES_OK
+    assert len(results) == 600
+    for r in results:
+        assert r["status"] == ca.CYAES_OK
+        aes = oracle.Rijndael(keys[r["k"]])
+        want = (aes.decrypt if r["op"] == ca.OP_DECRYPT else aes.encrypt)(bytearray(r["data"]))
+        assert bytes(r["out"]) == bytes(want)
+    st = batcher.stats()
+    assert st["pending"] == 0 and st["errors"] == 0 and st["batches"] >= 1
+    for s in slots:
+        batcher.session_close(s)
+
+
+def test_relay_seal_open_round_trip(batcher):
+    """SEAL = relay_local.cpp:189-206 (packet + 0xCE pad + encrypt); OPEN =
+    relay_server.cpp:329 (decrypt in place)."""
+    key = _keys(1, 2)[0]
+    slot = batcher.session_open(key)
+    rng = random.Random(3)
+    sizes = [0, 1, 15, 16, 17, 1472, 4095, 0xFF00] + [rng.randrange(1, 0xFF01) for _ in range(40)]
+    sealed = []
+    for i, n in enumerate(sizes):
+        chunk = bytes(rng.randrange(256) for _ in range(n))
+        pkt = bytearray(ca.relay_packet_bytes(n))
+        batcher.submit_seal(slot, 1000 + i, chunk, pkt)
+        sealed.append((chunk, pkt))
+    assert batcher.flush() == ca.CYAES_OK
+    for i, (chunk, pkt) in enumerate(sealed):
+        assert bytes(pkt) == ro.seal_forward(key, 1000 + i, chunk)
+    # the receive side: a stream of sealed packets, parsed and opened in place
+    stream = b"".join(bytes(p) for _, p in sealed)
+    parsed, used = ca.relay_parse(stream)
+    assert used == len(stream) and len(parsed) == len(sizes)
+    opened = [bytearray(stream[o:o + 4 + s]) for o, s, _ in parsed]
+    for p in opened:
+        batcher.submit_open(slot, p)
+    assert batcher.flush() == ca.CYAES_OK
+    for (chunk, spkt), p in zip(sealed, opened):
+        conn, payload, whole = ro.open_forward(key, bytes(spkt))
+        assert bytes(p) == whole and payload == chunk
+        size = struct.unpack("<i", bytes(p[8:12]))[0]
+        assert bytes(p[12:12 + size]) == chunk
+    batcher.session_close(slot)
+
+
+def test_session_reopen_and_errors(batcher):
+    k1, k2 = _keys(2, 4)
+    s = batcher.session_open(k1)
+    data = bytes(range(256)) * 4
+    out1 = bytearray(len(data))
+    batcher.submit(ca.OP_ENCRYPT, s, data, out1)
+    batcher.session_close(s)  # the submitted request keeps k1
+    s2 = batcher.session_open(k2)
+    assert s2 == s  # lowest free slot is reused
+    out2 = bytearray(len(data))
+    batcher.submit(ca.OP_ENCRYPT, s2, data, out2)
+    assert batcher.flush() == ca.CYAES_OK
+    assert bytes(out1) == bytes(oracle.Rijndael(k1).encrypt(bytearray(data)))
+    assert bytes(out2) == bytes(oracle.Rijndael(k2).encrypt(bytearray(data)))
+    with pytest.raises(ca.CyaesError) as e:
+        batcher.submit(ca.OP_ENCRYPT, s2, data, bytearray(len(data)), 17)
+    assert e.value.status == ca.CYAES_EINVAL
+    with pytest.raises(ca.CyaesError) as e:
+        batcher.submit(ca.OP_ENCRYPT, 999, data, bytearray(len(data)))
+    assert e.value.status == ca.CYAES_ERANGE
+    with pytest.raises(ca.CyaesError) as e:  # larger than a batch
+        big = bytes(8 << 20)
+        batcher.submit(ca.OP_ENCRYPT, s2, big, bytearray(len(big)))
+    assert e.value.status == ca.CYAES_EINVAL
+    bad = bytearray(ca.relay_build_forward(1, b"x" * 20))
+    bad[1] ^= 1  # packet_size no longer matches the buffer
+    with pytest.raises(ca.CyaesError):
+        batcher.submit_open(s2, bad)
+    batcher.session_close(s2)
+
+
+def test_large_requests_fill_several_batches():
+    b = ca.Batcher(0, max_batch_bytes=1 << 20, max_delay_us=50, inflight=2)
+    try:
+        key = _keys(1, 9)[0]
+        s = b.session_open(key)
+        rng = random.Random(9)
+        reqs = []
+        for i in range(24):
+            n = 16 * rng.randrange(1, 65536 // 16 * 8)  # up to 512 KiB
+            data = bytes(rng.getrandbits(8) for _ in range(n)) if i < 2 else bytes([i]) * n
+            out = bytearray(n)
+            b.submit(ca.OP_DECRYPT if i % 2 else ca.OP_ENCRYPT, s, data, out)
+            reqs.append((i, data, out))
+        assert b.flush() == ca.CYAES_OK
+        aes = oracle.Rijndael(key)
+        for i, data, out in reqs:
+            want = (aes.decrypt if i % 2 else aes.encrypt)(bytearray(data))
+            assert bytes(out) == bytes(want)
+        total = sum(len(d) for _, d, _ in reqs)
+        assert b.stats()["batches"] >= total // (1 << 20)  # no batch carries more than max_batch_bytes
+    finally:
+        b.close()
+
+
+def test_device_relay_stream_in_place():
+    """A connection's byte stream of relay packets, resident in HBM: the
+    payloads (packet offset 12, 4-byte aligned) are encrypted and decrypted
+    where they lie by the ragged kernels."""
+    import torch
+    key = _keys(1, 11)[0]
+    rng = random.Random(11)
+    chunks = [bytes(rng.randrange(256) for _ in range(rng.choice([1, 16, 100, 1472, 0xFF00, rng.randrange(1, 9000)])))
+              for _ in range(300)]
+    plain = b"".join(ro.seal_forward(None, i, c, encrypt=False) for i, c in enumerate(chunks))
+    sealed = b"".join(ro.seal_forward(key, i, c) for i, c in enumerate(chunks))
+    parsed, used = ca.relay_parse(plain)
+    assert used == len(plain)
+    off, ln = ca.relay_payloads(parsed)
+    assert any(o % 16 for o in off)  # genuinely misaligned payloads
+    ctx = ca.GpuContext(0)
+    ctx.set_keys(key)
+    dev = torch.frombuffer(bytearray(plain), dtype=torch.uint8).cuda()
+    d_off = torch.tensor(off, dtype=torch.int64).cuda()
+    d_len = torch.tensor(ln, dtype=torch.int32).cuda()
+    ctx.encrypt_ragged(dev, dev, d_off, d_len, len(off))
+    assert ctx.check() == ca.CYAES_OK
+    assert bytes(dev.cpu().numpy().tobytes()) == sealed
+    ctx.decrypt_ragged(dev, dev, d_off, d_len, len(off))
+    assert bytes(dev.cpu().numpy().tobytes()) == plain
+    # the SURVEY §8(b) batch entry points (per-payload input IV, key index)
+    lib = ca.load_library()
+    ivs = torch.frombuffer(bytearray(bytes(range(16)) * len(off)), dtype=torch.uint8).cuda()
+    kid = torch.zeros(len(off), dtype=torch.int32).cuda()
+    out = torch.empty_like(dev)
+    assert lib.cyaes_gpu_cbc_encrypt_batch(ctx._h, dev.data_ptr(), out.data_ptr(), d_off.data_ptr(),
+                                           d_len.data_ptr(), kid.data_ptr(), ivs.data_ptr(), len(off), None) == 0
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().tobytes()
+    for o, n in zip(off, ln):
+        assert got[o:o + n] == sealed[o:o + n]
+    ctx.close()
+
+
+def test_update_keys_partial():
+    import torch
+    ctx = ca.GpuContext(0)
+    keys = _keys(5, 12)
+    ctx.set_keys(b"".join(keys[:3]))
+    new = _keys(3, 13)
+    lib = ca.load_library()
+    buf = (ca.ctypes.c_uint8 * 48).from_buffer_copy(b"".join(new))
+    assert lib.cyaes_gpu_update_keys(ctx._h, 2, buf, 3) == 0  # replaces row 2, appends 3..4
+    assert ctx.nkeys == 5
+    table = [keys[0], keys[1], new[0], new[1], new[2]]
+    for i, k in enumerate(table):
+        assert ctx.get_key(i).words() == oracle.key_expand(k).words()
+    assert lib.cyaes_gpu_update_keys(ctx._h, 6, buf, 1) == ca.CYAES_EINVAL  # first > nkeys
+    data = torch.arange(5 * 256, dtype=torch.int32).to(torch.uint8).cuda()
+    out = torch.empty_like(data)
+    ctx.encrypt_uniform(data, out, 5, 256, payloads_per_key=1)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().tobytes()
+    src = data.cpu().numpy().tobytes()
+    for p, k in enumerate(table):
+        assert got[256 * p:256 * (p + 1)] == bytes(oracle.Rijndael(k).encrypt(bytearray(src[256 * p:256 * (p + 1)])))
+    ctx.close()

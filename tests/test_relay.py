@@ -1,0 +1,88 @@
+"""Relay wire format (include/cyaes_relay.h) against the
+restatement of the reference relay in oracle/relay_oracle.py.  Host logic
+only: no GPU."""
+import random
+import struct
+
+import pytest
+
+import cyclone_amd as ca
+import relay_oracle as ro
+
+SIZES = [0, 1, 15, 16, 17, 31, 1400, 1472, 4095, 0xFEFF, 0xFF00]
+
+
+def test_round16_and_packet_bytes():
+    lib = ca.load_library()
+    for n in list(range(0, 70)) + SIZES:
+        assert lib.cyaes_relay_round16(n) == ro.round16(n)
+        assert ca.relay_packet_bytes(n) == 12 + ro.round16(n)
+
+
+@pytest.mark.parametrize("size", SIZES)
+def test_build_forward_matches_reference_packet(size):
+    rng = random.Random(size)
+    chunk = bytes(rng.randrange(256) for _ in range(size))
+    conn = rng.randrange(-2**31, 2**31)
+    assert ca.relay_build_forward(conn, chunk) == ro.seal_forward(None, conn, chunk, encrypt=False)
+    pkt = ca.relay_build_forward(conn, chunk)
+    lib = ca.load_library()
+    buf = (ca.ctypes.c_uint8 * len(pkt)).from_buffer_copy(pkt)
+    assert lib.cyaes_relay_forward_id(buf) == conn and lib.cyaes_relay_forward_size(buf) == size
+    assert struct.unpack(">HH", pkt[:4]) == (8 + ro.round16(size), ro.RELAY_FORWARD)
+
+
+def test_build_forward_rejects_oversize_chunk():
+    with pytest.raises(ValueError):
+        ca.relay_build_forward(1, bytes(0xFF01))
+    lib = ca.load_library()
+    assert lib.cyaes_relay_build_forward(None, 1, None, 0) == 0
+
+
+def _stream(rng, n):
+    pkts = []
+    for _ in range(n):
+        if rng.random() < 0.2:  # other relay messages share the connection (relay_protocol.h:9-14)
+            pid = rng.choice([ro.RELAY_HANDSHAKE_ID, ro.RELAY_HANDSHAKE_ID + 1, ro.RELAY_HANDSHAKE_ID + 2])
+            pkts.append(bytes(ro.build_packet(4, pid, struct.pack("<i", rng.randrange(1000)))))
+        else:
+            size = rng.choice(SIZES + [rng.randrange(1, 3000)])
+            pkts.append(ro.seal_forward(None, rng.randrange(100), bytes(rng.randrange(256) for _ in range(size)),
+                                        encrypt=False))
+    return pkts
+
+
+def test_parse_matches_reference_incl_incomplete_tail():
+    rng = random.Random(5)
+    pkts = _stream(rng, 60)
+    stream = b"".join(pkts)
+    for cut in [len(stream), len(stream) - 1, len(stream) - len(pkts[-1]), 3, 0, 4]:
+        got, used = ca.relay_parse(stream[:cut])
+        want, wused = ro.parse_stream(stream[:cut])
+        assert got == want and used == wused
+
+
+def test_payloads_select_forward_packets():
+    rng = random.Random(6)
+    pkts = _stream(rng, 40)
+    stream = b"".join(pkts)
+    parsed, _ = ca.relay_parse(stream)
+    off, ln = ca.relay_payloads(parsed, base=1000)
+    want = [(1000 + o + 12, s - 8) for o, s, i in parsed if i == ro.RELAY_FORWARD and s > 8]
+    assert list(zip(off, ln)) == want
+    assert all(o % 4 == 0 for o in off) and all(x % 16 == 0 for x in ln)
+    bad = [(0, 8 + 17, ro.RELAY_FORWARD)]  # a payload the reference encrypt path cannot produce
+    with pytest.raises(ValueError):
+        ca.relay_payloads(bad)
+
+
+def test_batcher_without_device_fails_loudly():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("checks the no-device path")
+    except ImportError:
+        pass
+    with pytest.raises(ca.CyaesError) as e:
+        ca.Batcher(0)
+    assert e.value.status == ca.CYAES_ENODEV
