@@ -24,7 +24,7 @@ KOBJ     := $(BUILD)/cyaes_kernels.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
 .PHONY: all lib oracle cpptest microbench variant clean
-all: lib oracle cpptest
+all: lib oracle cpptest $(BUILD)/bench_batcher
 lib: $(LIB)
 oracle: $(ORACLE)
 cpptest: $(CPPTEST)
@@ -47,7 +47,10 @@ $(ORACLE): oracle/aes_oracle.c
 $(CPPTEST): tests/cpp/test_rijndael.cpp $(LIB) $(HDRS)
 	$(CXX) -O2 -std=c++17 -Wall $(INC) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
 
-microbench: $(BUILD)/microbench
+microbench: $(BUILD)/microbench $(BUILD)/bench_batcher
+
+$(BUILD)/bench_batcher: tools/bench_batcher.cpp $(LIB) $(HDRS) | $(BUILD)
+	$(CXX) -O2 -std=c++17 -Wall -pthread $(INC) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
 
 $(BUILD)/microbench: tools/microbench.hip | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -o $@ $<

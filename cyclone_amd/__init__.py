@@ -127,6 +127,14 @@ def load_library(path=LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise ImportError("cyclone_amd: %s is not built (run `make` or __graft_entry__.build())" % path)
+    # PyTorch-ROCm bundles its own libamdhip64 (soname libamdhip64.so.7, like
+    # /opt/rocm's).  Loaded first, it satisfies libcyaes.so's dependency and the
+    # process has one HIP runtime; loaded after ours, torch would map a second
+    # runtime and find no GPU.  So let torch (if present) load first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)

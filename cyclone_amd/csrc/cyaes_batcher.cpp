@@ -189,6 +189,40 @@ int cyaes_batcher::launch(Stage* st) {
         (dec ? dk : ek).push_back(k);
     }
     st->data_end = pos;
+    // Encrypt runs one chain per lane and waterfalls over the distinct keys of
+    // a wave (cyaes_kernels.hip, k_encrypt), so order its list by key: a wave
+    // then sees one key, two at a boundary, instead of one per looper thread.
+    // (Decrypt runs one payload per wave: one key per wave already.)
+    if (klist.size() > 1 && !eo.empty()) {
+        std::vector<uint32_t> ord(eo.size());
+        for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return ek[x] < ek[y]; });
+        std::vector<uint64_t> o2(eo.size());
+        std::vector<uint32_t> l2(el.size()), k2(ek.size());
+        for (size_t i = 0; i < ord.size(); i++) o2[i] = eo[ord[i]], l2[i] = el[ord[i]], k2[i] = ek[ord[i]];
+        // Small batch: start every key group on a wave boundary with empty
+        // (0-byte) lanes, so no wave waterfalls; the waves are then all
+        // latency-bound chains on separate CUs (A/B on bench_batcher seal 1472 B).
+        uint64_t waves = 0;
+        for (size_t i = 0; i < k2.size();) {
+            size_t j = i;
+            while (j < k2.size() && k2[j] == k2[i]) j++;
+            waves += (j - i + 63) / 64;
+            i = j;
+        }
+        if (waves <= 4096) {
+            eo.clear(), el.clear(), ek.clear();
+            for (size_t i = 0; i < k2.size(); i++) {
+                if (i && k2[i] != k2[i - 1])
+                    while (eo.size() % 64) eo.push_back(0), el.push_back(0), ek.push_back(k2[i - 1]);
+                eo.push_back(o2[i]), el.push_back(l2[i]), ek.push_back(k2[i]);
+            }
+        } else {
+            eo.swap(o2);
+            el.swap(l2);
+            ek.swap(k2);
+        }
+    }
     // Meta + keys after the data.
     auto put = [&](const void* src, size_t bytes) {
         const uint64_t at = pos;

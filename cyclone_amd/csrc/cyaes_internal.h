@@ -93,9 +93,9 @@ struct DecArgs {
 };
 
 // Launchers (cyaes_kernels.hip).  All asynchronous on `stream`.
-hipError_t launch_encrypt(const EncArgs& a, int grid, hipStream_t stream);
+hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t stream);
 hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream);
-hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, hipStream_t stream);
+hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, int threads, hipStream_t stream);
 hipError_t launch_boundary_snapshot(const uint8_t* in, uint64_t nblocks, uint64_t blocks_per_wave,
                                     uint64_t nwaves, Fastdiv bpp, uint4* boundary, hipStream_t stream);
 hipError_t launch_key_expand(const uint8_t* d_keys, uint32_t nkeys, const uint8_t* d_sbox,

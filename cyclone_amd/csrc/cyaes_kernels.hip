@@ -191,13 +191,13 @@ __device__ __forceinline__ uint32_t dec_last(const char* lds, uint32_t lo, uint3
 }
 __device__ __forceinline__ void fill_dec_image(uint32_t* lds, const uint32_t* __restrict__ t) {
     uint4* l4 = reinterpret_cast<uint4*>(lds);
-    for (int q = threadIdx.x; q < 8192; q += kDecThreads) {  // two 64 KiB T regions
+    for (int q = threadIdx.x; q < 8192; q += blockDim.x) {  // two 64 KiB T regions
         const int region = q >> 12, half = (q >> 3) & 1, row = (q >> 4) & 255;
         uint32_t v = t[256 * region + row];
         if (half) v = rotl8(v);
         l4[q] = make_uint4(v, v, v, v);
     }
-    for (int q = threadIdx.x; q < 2048; q += kDecThreads) {  // Si: 256 rows x 128 B
+    for (int q = threadIdx.x; q < 2048; q += blockDim.x) {  // Si: 256 rows x 128 B
         const uint32_t v = t[512 + (q >> 3)];
         l4[8192 + q] = make_uint4(v, v, v, v);
     }
@@ -361,8 +361,8 @@ __device__ __forceinline__ void drain_loads() { asm volatile("s_waitcnt vmcnt(0)
 template <bool RAGGED, bool KEYED>
 __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
-    fill_region(lds_words, a.tables, a.tables + 256, kEncThreads);
-    fill_region(lds_words + 16384, a.tables + 512, a.tables + 768, kEncThreads);
+    fill_region(lds_words, a.tables, a.tables + 256, blockDim.x);
+    fill_region(lds_words + 16384, a.tables + 512, a.tables + 768, blockDim.x);
     __shared__ uint32_t lead;  // prio_feedback
     if (threadIdx.x == 0) lead = 0;
     uint32_t prog = 0;
@@ -371,8 +371,10 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
-    const uint64_t wstride = (uint64_t)gridDim.x * kEncThreads;
-    const uint64_t wbase0 = (uint64_t)blockIdx.x * kEncThreads + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+    // Block size: kEncThreads for big batches; fewer for small ones, so that
+    // few chains spread over many CUs (cyaes_runtime.cpp, small_grid).
+    const uint64_t wstride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t wbase0 = (uint64_t)blockIdx.x * blockDim.x + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
 
     for (uint64_t wbase = wbase0; wbase < a.npayloads; wbase += wstride) {
         const uint64_t p = wbase + lane;
@@ -451,89 +453,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     }
 }
 
-#if CYAES_ENC2  // A/B variant (tools/ab.py): measured ~1% slower than k_encrypt on config C
-// ---- CBC encrypt, uniform single-key batch: two chains per lane ----------
-// Lane l of a wave owns payloads wbase+l and wbase+64+l and advances both
-// chains together (2-way ILP per LDS round trip).  Same semantics as k_encrypt.
-constexpr int kEnc2Threads = 512;
-__global__ __launch_bounds__(kEnc2Threads, 1) void k_encrypt2(EncArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
-    fill_region(lds_words, a.tables, a.tables + 256, kEnc2Threads);
-    fill_region(lds_words + 16384, a.tables + 512, a.tables + 768, kEnc2Threads);
-    __syncthreads();
-    const char* lds = reinterpret_cast<const char*>(lds_words);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
-    const uint64_t wstride = (uint64_t)gridDim.x * kEnc2Threads * 2;
-    const uint64_t wbase0 =
-        (uint64_t)blockIdx.x * kEnc2Threads * 2 + 2 * __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
-    uint32_t ek[44];
-    load_sched(a.keys.table, ek);
-    const uint32_t nb = a.payload_bytes >> 4;
-    for (uint64_t wbase = wbase0; wbase < a.npayloads; wbase += wstride) {
-        uint64_t p[2] = {wbase + lane, wbase + 64 + lane};
-        const bool act[2] = {p[0] < a.npayloads, p[1] < a.npayloads};
-        if (!act[1]) p[1] = act[0] ? p[0] : 0;  // duplicate work, never stored
-        if (!act[0]) p[0] = 0;
-        uint4 c[2];
-#pragma unroll
-        for (int n = 0; n < 2; n++) c[n] = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p[n]) : default_iv();
-        const uint4* src[2] = {reinterpret_cast<const uint4*>(a.in + p[0] * a.payload_bytes),
-                               reinterpret_cast<const uint4*>(a.in + p[1] * a.payload_bytes)};
-        uint4* dst[2] = {reinterpret_cast<uint4*>(a.out + p[0] * a.payload_bytes),
-                         reinterpret_cast<uint4*>(a.out + p[1] * a.payload_bytes)};
-        uint32_t i = 0;
-        for (; i + 4 <= nb; i += 4) {
-            uint4 b[2][4];
-#pragma unroll
-            for (int n = 0; n < 2; n++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) b[n][j] = src[n][i + j];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                uint32_t st[2][4];
-#pragma unroll
-                for (int n = 0; n < 2; n++) {
-                    st[n][0] = xor3(c[n].x, b[n][j].x, ek[0]); st[n][1] = xor3(c[n].y, b[n][j].y, ek[1]);
-                    st[n][2] = xor3(c[n].z, b[n][j].z, ek[2]); st[n][3] = xor3(c[n].w, b[n][j].w, ek[3]);
-                }
-                enc_blocks<2>(lds, lo, ek, st);
-#pragma unroll
-                for (int n = 0; n < 2; n++) {
-                    c[n] = make_uint4(st[n][0], st[n][1], st[n][2], st[n][3]);
-                    b[n][j] = c[n];
-                }
-            }
-#pragma unroll
-            for (int n = 0; n < 2; n++)
-                if (act[n]) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) dst[n][i + j] = b[n][j];
-                }
-        }
-        for (; i < nb; i++) {
-            uint32_t st[2][4];
-#pragma unroll
-            for (int n = 0; n < 2; n++) {
-                const uint4 v = src[n][i];
-                st[n][0] = xor3(c[n].x, v.x, ek[0]); st[n][1] = xor3(c[n].y, v.y, ek[1]);
-                st[n][2] = xor3(c[n].z, v.z, ek[2]); st[n][3] = xor3(c[n].w, v.w, ek[3]);
-            }
-            enc_blocks<2>(lds, lo, ek, st);
-#pragma unroll
-            for (int n = 0; n < 2; n++) {
-                c[n] = make_uint4(st[n][0], st[n][1], st[n][2], st[n][3]);
-                if (act[n]) dst[n][i] = c[n];
-            }
-        }
-        if (a.iv_out) {
-#pragma unroll
-            for (int n = 0; n < 2; n++)
-                if (act[n]) *reinterpret_cast<uint4*>(a.iv_out + 16 * p[n]) = c[n];
-        }
-    }
-}
-#endif  // CYAES_ENC2
+
 
 // ---- CBC decrypt, uniform contiguous batch: one lane per block ------------
 // The batch is one array of nblocks blocks; payload boundaries every bpp
@@ -770,9 +690,9 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lo = dec_lo(threadIdx.x);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kDecThreads / 64);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
     const uint64_t wave0 =
-        (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        (uint64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (uint64_t p = wave0; p < a.npayloads; p += nwaves) {
         const uint8_t* in = a.in + a.offsets[p];  // 4-B aligned
         uint8_t* out = a.out + a.offsets[p];
@@ -913,18 +833,10 @@ __global__ void k_digest(const uint64_t* buf, uint64_t nwords, unsigned long lon
 
 }  // namespace
 
-hipError_t launch_encrypt(const EncArgs& a, int grid, hipStream_t stream) {
+hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
     const bool ragged = a.offsets != nullptr;
-#if CYAES_ENC2
-    if (!ragged && !keyed) {
-        const uint64_t want = (a.npayloads + 2 * kEnc2Threads - 1) / (2 * kEnc2Threads);
-        const int g2 = (int)(want < (uint64_t)grid ? want : (uint64_t)grid);
-        hipLaunchKernelGGL(k_encrypt2, dim3(g2 > 0 ? g2 : 1), dim3(kEnc2Threads), 0, stream, a);
-        return hipGetLastError();
-    }
-#endif
-    const dim3 g(grid), b(kEncThreads);
+    const dim3 g(grid), b(threads);
     if (ragged && keyed) hipLaunchKernelGGL((k_encrypt<true, true>), g, b, 0, stream, a);
     else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false>), g, b, 0, stream, a);
     else if (keyed) hipLaunchKernelGGL((k_encrypt<false, true>), g, b, 0, stream, a);
@@ -943,8 +855,8 @@ hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, hipStream_t stream) {
-    hipLaunchKernelGGL(k_decrypt_ragged, dim3(grid), dim3(kDecThreads), 0, stream, a);
+hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, int threads, hipStream_t stream) {
+    hipLaunchKernelGGL(k_decrypt_ragged, dim3(grid), dim3(threads), 0, stream, a);
     return hipGetLastError();
 }
 

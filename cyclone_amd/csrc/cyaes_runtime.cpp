@@ -91,6 +91,22 @@ int make_keysel(const cyaes_gpu* ctx, uint64_t npayloads, const uint32_t* key_id
 int enc_grid_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kEncWgPerCu); }
 int dec_grid_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kDecWgPerCu); }
 
+// Launch shape for `waves` independent wave-sized work items (encrypt: 64
+// chains; ragged decrypt: one payload).  Enough to fill every CU with 16
+// waves: full 1024-thread workgroups, grid capped at one per CU (persistent).
+// Fewer: spread them, ceil(waves / CUs) waves per workgroup, so a small
+// batch of serial chains runs on many CUs' LDS instead of queueing on one.
+struct Shape {
+    int grid, threads;
+};
+Shape wave_shape(const cyaes_gpu* ctx, uint64_t waves, int max_threads) {
+    const uint64_t cus = (uint64_t)std::max(1, ctx->num_cus);
+    const uint64_t per_wg = (uint64_t)max_threads / 64;
+    if (waves >= cus * per_wg) return {(int)cus, max_threads};
+    const uint64_t w = std::max<uint64_t>(1, (waves + cus - 1) / cus);
+    return {(int)std::max<uint64_t>(1, (waves + w - 1) / w), (int)(64 * w)};
+}
+
 int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
                    uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk,
                    const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream, const uint32_t* table = nullptr,
@@ -108,10 +124,9 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.iv_out = iv_out;
     a.tables = ctx->d_tables + kEncTableOff / 4;
     a.status = ctx->d_status;
-    const uint64_t want = (npayloads + kEncThreads - 1) / kEncThreads;
-    const int grid = (int)std::min<uint64_t>(want, (uint64_t)enc_grid_cap(ctx));
+    const Shape sh = wave_shape(ctx, (npayloads + 63) / 64, kEncThreads);
     ctx->last_stream = stream;
-    return map_err(launch_encrypt(a, grid, stream));
+    return map_err(launch_encrypt(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
 }
 
 // d_iv_in == d_iv_out on a block-parallel decrypt: a payload's last block may
@@ -184,10 +199,9 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.tables = ctx->d_tables + kDecTableOff / 4;
     a.status = ctx->d_status;
     a.inplace = in == out;
-    constexpr int kWaves = kDecThreads / 64;
-    const int grid = (int)std::min<uint64_t>((npayloads + kWaves - 1) / kWaves, (uint64_t)dec_grid_cap(ctx));
+    const Shape sh = wave_shape(ctx, npayloads, kDecThreads);
     ctx->last_stream = stream;
-    return map_err(launch_decrypt_ragged(a, grid, stream));
+    return map_err(launch_decrypt_ragged(a, std::min(sh.grid, dec_grid_cap(ctx)), sh.threads, stream));
 }
 
 bool aligned4(const void* p) { return ((uintptr_t)p & 3u) == 0; }

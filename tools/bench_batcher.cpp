@@ -1,0 +1,207 @@
+// tools/bench_batcher.cpp -- relay-shaped load on the batching adapter
+// (include/cyaes_batch.h), host to host (PCIe-inclusive).
+//
+// T "looper" threads each keep W requests in flight on their own session and
+// resubmit from the completion callback's slot as soon as one finishes, the
+// way a relay pipe would seal every chunk it reads (relay_local.cpp:189-206)
+// or open every packet it receives (relay_server.cpp:329).  Reports requests/s,
+// payload GiB/s and submit->callback latency percentiles as one JSON line, and
+// for comparison the synchronous drop-in path (cyaes_cbc_encrypt, one packet
+// per call, as the reference calls Rijndael::encrypt).
+//
+// usage: bench_batcher [--op seal|open|enc|dec] [--size B] [--threads T]
+//                      [--window W] [--seconds S] [--batch-mb M] [--delay-us D]
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "cyaes.h"
+#include "cyaes_batch.h"
+#include "cyaes_relay.h"
+
+using Clock = std::chrono::steady_clock;
+
+struct Slot {
+    std::vector<uint8_t> in, out;
+    Clock::time_point t0;
+    struct Looper* owner = nullptr;
+};
+
+struct Looper {
+    cyaes_batcher* b = nullptr;
+    uint32_t session = 0;
+    int op = CYAES_OP_RELAY_SEAL;
+    uint32_t size = 1472;
+    std::vector<Slot> slots;
+    std::mutex mu;
+    std::vector<Slot*> ready;  // completed, to resubmit
+    std::vector<double> lat_us;
+    std::atomic<uint64_t> done{0};
+    int err = 0;
+};
+
+static void on_done(void* user, int status) {
+    Slot* s = static_cast<Slot*>(user);
+    Looper* L = s->owner;
+    const double us = std::chrono::duration<double, std::micro>(Clock::now() - s->t0).count();
+    std::lock_guard<std::mutex> lk(L->mu);
+    if (status) L->err = status;
+    if (L->lat_us.size() < 2000000) L->lat_us.push_back(us);
+    L->ready.push_back(s);
+    L->done.fetch_add(1, std::memory_order_relaxed);
+}
+
+static int submit(Looper* L, Slot* s) {
+    s->t0 = Clock::now();
+    switch (L->op) {
+        case CYAES_OP_RELAY_SEAL:
+            return cyaes_batcher_submit_seal(L->b, L->session, 7, s->in.data(), L->size, s->out.data(), on_done, s);
+        case CYAES_OP_RELAY_OPEN:  // re-open the same sealed packet: the work is the same every time
+            memcpy(s->out.data(), s->in.data(), s->in.size());
+            return cyaes_batcher_submit_open(L->b, L->session, s->out.data(), (uint32_t)s->out.size(), on_done, s);
+        default:
+            return cyaes_batcher_submit(L->b, L->op, L->session, s->in.data(), s->out.data(), L->size, on_done, s);
+    }
+}
+
+static double pct(std::vector<double>& v, double p) {
+    if (v.empty()) return 0;
+    size_t k = std::min(v.size() - 1, (size_t)(p * (v.size() - 1)));
+    std::nth_element(v.begin(), v.begin() + k, v.end());
+    return v[k];
+}
+
+int main(int argc, char** argv) {
+    std::string op = "seal";
+    uint32_t size = 1472, threads = 8, window = 512, batch_mb = 32, delay_us = 100;
+    double seconds = 5;
+    for (int i = 1; i + 1 < argc; i += 2) {
+        std::string a = argv[i];
+        if (a == "--op") op = argv[i + 1];
+        else if (a == "--size") size = atoi(argv[i + 1]);
+        else if (a == "--threads") threads = atoi(argv[i + 1]);
+        else if (a == "--window") window = atoi(argv[i + 1]);
+        else if (a == "--seconds") seconds = atof(argv[i + 1]);
+        else if (a == "--batch-mb") batch_mb = atoi(argv[i + 1]);
+        else if (a == "--delay-us") delay_us = atoi(argv[i + 1]);
+    }
+    const int opc = op == "seal" ? CYAES_OP_RELAY_SEAL : op == "open" ? CYAES_OP_RELAY_OPEN
+                    : op == "dec" ? CYAES_OP_DECRYPT : CYAES_OP_ENCRYPT;
+    if ((opc == CYAES_OP_ENCRYPT || opc == CYAES_OP_DECRYPT) && size % 16) size = cyaes_relay_round16(size);
+    if (opc >= CYAES_OP_RELAY_SEAL && size > CYAES_RELAY_MAX_CHUNK) size = CYAES_RELAY_MAX_CHUNK;
+
+    cyaes_batcher_config cfg = {0, batch_mb << 20, delay_us, 3};
+    cyaes_batcher* b = nullptr;
+    int st = cyaes_batcher_create(&cfg, &b);
+    if (st) {
+        fprintf(stderr, "cyaes_batcher_create: %s\n", cyaes_strerror(st));
+        return 1;
+    }
+    std::vector<Looper> loopers(threads);
+    for (uint32_t t = 0; t < threads; t++) {
+        Looper& L = loopers[t];
+        L.b = b;
+        L.op = opc;
+        L.size = size;
+        uint8_t key[16];
+        for (int i = 0; i < 16; i++) key[i] = (uint8_t)(t * 16 + i);
+        cyaes_batcher_session_open(b, key, &L.session);
+        L.slots.resize(window);
+        for (uint32_t w = 0; w < window; w++) {
+            Slot& s = L.slots[w];
+            s.owner = &L;
+            const uint32_t pkt = cyaes_relay_packet_bytes(size);
+            s.in.resize(opc == CYAES_OP_RELAY_OPEN ? pkt : size);
+            s.out.resize(opc >= CYAES_OP_RELAY_SEAL ? pkt : size);
+            for (size_t i = 0; i < s.in.size(); i++) s.in[i] = (uint8_t)(i * 131 + w);
+            if (opc == CYAES_OP_RELAY_OPEN) cyaes_relay_build_forward(s.in.data(), 7, s.in.data() + 12, size);
+        }
+    }
+    // Warm-up: one window per looper.
+    for (auto& L : loopers)
+        for (auto& s : L.slots) submit(&L, &s);
+    cyaes_batcher_flush(b);
+    for (auto& L : loopers) {
+        L.ready.clear();
+        L.lat_us.clear();
+        L.done = 0;
+    }
+    uint64_t st0[6];
+    cyaes_batcher_stats(b, st0);
+
+    std::atomic<bool> stop{false};
+    const auto t0 = Clock::now();
+    std::vector<std::thread> th;
+    for (auto& L : loopers) {
+        th.emplace_back([&L, &stop] {
+            for (auto& s : L.slots) submit(&L, &s);
+            std::vector<Slot*> again;
+            while (!stop.load(std::memory_order_relaxed)) {
+                {
+                    std::lock_guard<std::mutex> lk(L.mu);
+                    again.swap(L.ready);
+                }
+                if (again.empty()) {
+                    std::this_thread::sleep_for(std::chrono::microseconds(20));
+                    continue;
+                }
+                for (Slot* s : again) submit(&L, s);
+                again.clear();
+            }
+        });
+    }
+    std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+    stop = true;
+    for (auto& t : th) t.join();
+    const uint64_t counted = [&] {
+        uint64_t n = 0;
+        for (auto& L : loopers) n += L.done.load();
+        return n;
+    }();
+    const double el = std::chrono::duration<double>(Clock::now() - t0).count();
+    cyaes_batcher_flush(b);
+    uint64_t st1[6];
+    cyaes_batcher_stats(b, st1);
+    std::vector<double> lat;
+    int err = 0;
+    for (auto& L : loopers) {
+        lat.insert(lat.end(), L.lat_us.begin(), L.lat_us.end());
+        err |= L.err;
+    }
+    const double payload = (double)(opc >= CYAES_OP_RELAY_SEAL ? cyaes_relay_round16(size) : size);
+    const double batches = (double)(st1[1] - st0[1]);
+    const double p50 = pct(lat, 0.5), p99 = pct(lat, 0.99);
+    cyaes_batcher_destroy(b);
+
+    // Synchronous drop-in for comparison: one packet per call (relay_local.cpp:206 shape).
+    cyaes_key k;
+    uint8_t key[16] = {0};
+    cyaes_key_expand(key, &k);
+    std::vector<uint8_t> buf(cyaes_relay_round16(size));
+    cyaes_cbc_encrypt(&k, buf.data(), buf.data(), buf.size(), nullptr);
+    int calls = 0;
+    const auto s0 = Clock::now();
+    while (std::chrono::duration<double>(Clock::now() - s0).count() < 1.0) {
+        cyaes_cbc_encrypt(&k, buf.data(), buf.data(), buf.size(), nullptr);
+        calls++;
+    }
+    const double sync_s = std::chrono::duration<double>(Clock::now() - s0).count();
+
+    printf("{\"metric\": \"batcher %s requests/s host-to-host\", \"op\": \"%s\", \"size\": %u, \"threads\": %u, "
+           "\"window\": %u, \"batch_mb\": %u, \"delay_us\": %u, \"seconds\": %.2f, \"requests\": %llu, "
+           "\"requests_per_s\": %.0f, \"payload_gibs\": %.3f, \"mean_batch\": %.1f, \"lat_p50_us\": %.0f, "
+           "\"lat_p99_us\": %.0f, \"errors\": %d, \"sync_dropin_calls_per_s\": %.0f, "
+           "\"sync_dropin_gibs\": %.4f}\n",
+           op.c_str(), op.c_str(), size, threads, window, batch_mb, delay_us, el, (unsigned long long)counted,
+           counted / el, counted * payload / el / (1u << 30), batches > 0 ? (st1[0] - st0[0]) / batches : 0.0, p50,
+           p99, err, calls / sync_s, calls * (double)buf.size() / sync_s / (1u << 30));
+    return err ? 2 : 0;
+}
