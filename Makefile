@@ -11,6 +11,7 @@ HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 HOSTFLAGS:= -O2 -std=c++17 -fPIC -Wall $(INC) -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
 
 LIB      := cyclone_amd/libcyaes.so
+MGPU     := cyclone_amd/libcyaes_mgpu.so
 ORACLE   := oracle/liboracle.so
 CPPTEST  := $(BUILD)/test_rijndael
 
@@ -23,9 +24,10 @@ HDRS     := include/cyaes.h include/cyaes_relay.h include/cyaes_batch.h include/
 KOBJ     := $(BUILD)/cyaes_kernels.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
-.PHONY: all lib oracle cpptest microbench variant clean
-all: lib oracle cpptest $(BUILD)/bench_batcher
+.PHONY: all lib mgpu oracle cpptest microbench variant clean
+all: lib mgpu oracle cpptest $(BUILD)/bench_batcher
 lib: $(LIB)
+mgpu: $(MGPU)
 oracle: $(ORACLE)
 cpptest: $(CPPTEST)
 
@@ -40,6 +42,10 @@ $(BUILD)/%.o: cyclone_amd/csrc/%.cpp $(HDRS) | $(BUILD)
 
 $(LIB): $(KOBJ) $(HOBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
+
+# Single-process multi-GPU front end: separate library so libcyaes.so does not pull in RCCL.
+$(MGPU): cyclone_amd/csrc/cyaes_mgpu.cpp include/cyaes_mgpu.h $(LIB)
+	$(HIPCC) $(HOSTFLAGS) -shared -o $@ $< -Lcyclone_amd -lcyaes -L/opt/rocm/lib -lrccl -Wl,-rpath,'$$ORIGIN'
 
 $(ORACLE): oracle/aes_oracle.c
 	$(CC) -O2 -fPIC -shared -pthread -Wall -o $@ $<
@@ -62,4 +68,4 @@ variant: $(HOBJ) | $(BUILD)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/$(NAME).so $(BUILD)/variants/$(NAME).o $(HOBJ)
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(ORACLE)
+	rm -rf $(BUILD) $(LIB) $(MGPU) $(ORACLE)

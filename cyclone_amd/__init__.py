@@ -109,6 +109,8 @@ _lib = None
 
 HEADERS = [os.path.join(os.path.dirname(_HERE), "include", h)
            for h in ("cyaes.h", "cyaes_relay.h", "cyaes_batch.h")]
+MGPU_HEADER = os.path.join(os.path.dirname(_HERE), "include", "cyaes_mgpu.h")
+MGPU_LIB_PATH = os.path.join(_HERE, "libcyaes_mgpu.so")
 
 
 def header_functions(paths=None):
@@ -494,3 +496,89 @@ class Batcher:
         _check(self._lib.cyaes_batcher_stats(self._h, out), "stats")
         keys = ("completed", "batches", "bytes", "max_batch", "errors", "pending")
         return dict(zip(keys, (int(v) for v in out)))
+
+
+# ---- single-process multi-GPU (include/cyaes_mgpu.h, libcyaes_mgpu.so) -----
+_MGPU_SIGS = {
+    "cyaes_mgpu_create": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.POINTER(_vp)]),
+    "cyaes_mgpu_destroy": (None, [_vp]),
+    "cyaes_mgpu_ndev": (ctypes.c_int, [_vp]),
+    "cyaes_mgpu_context": (_vp, [_vp, ctypes.c_int]),
+    "cyaes_mgpu_broadcast_keys": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, ctypes.c_int]),
+    "cyaes_mgpu_shard": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, _u64p, _u64p]),
+    "cyaes_mgpu_encrypt_uniform": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32]),
+    "cyaes_mgpu_decrypt_uniform": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32]),
+}
+_mgpu_lib = None
+
+
+def load_mgpu_library(path=MGPU_LIB_PATH):
+    """Loads libcyaes_mgpu.so (RCCL); fails loudly if it is not built."""
+    global _mgpu_lib
+    if _mgpu_lib is not None:
+        return _mgpu_lib
+    load_library()  # torch first, then libcyaes.so (see load_library)
+    if not os.path.exists(path):
+        raise ImportError("cyclone_amd: %s is not built (run `make`)" % path)
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _MGPU_SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _mgpu_lib = lib
+    return lib
+
+
+def mgpu_shard(total, ndev, i, align=1):
+    first, count = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(load_mgpu_library().cyaes_mgpu_shard(total, ndev, i, align, ctypes.byref(first), ctypes.byref(count)),
+           "cyaes_mgpu_shard")
+    return first.value, count.value
+
+
+class MultiGpu:
+    """cyaes_mgpu: one context per device + an RCCL clique for key broadcast."""
+
+    def __init__(self, devices):
+        self._lib = load_mgpu_library()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = _vp()
+        _check(self._lib.cyaes_mgpu_create(len(devices), devs, ctypes.byref(h)), "cyaes_mgpu_create")
+        self._h = h
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.cyaes_mgpu_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ndev(self):
+        return self._lib.cyaes_mgpu_ndev(self._h)
+
+    def broadcast_keys(self, keys, root=0):
+        keys = bytes(keys)
+        buf = (ctypes.c_uint8 * len(keys)).from_buffer_copy(keys)
+        _check(self._lib.cyaes_mgpu_broadcast_keys(self._h, buf, len(keys) // 16, root), "broadcast_keys")
+
+    def _run(self, fn, d_in, d_out, npayloads, first, payload_bytes, ppk):
+        n = len(self.devices)
+        ins = (_vp * n)(*[_p(x) for x in d_in])
+        outs = (_vp * n)(*[_p(x) for x in d_out])
+        cnt = (ctypes.c_uint64 * n)(*npayloads)
+        fst = (ctypes.c_uint64 * n)(*(first or [0] * n))
+        _check(fn(self._h, ins, outs, cnt, fst, payload_bytes, ppk), fn.__name__)
+
+    def encrypt_uniform(self, d_in, d_out, npayloads, first, payload_bytes, payloads_per_key=0):
+        self._run(self._lib.cyaes_mgpu_encrypt_uniform, d_in, d_out, npayloads, first, payload_bytes,
+                  payloads_per_key)
+
+    def decrypt_uniform(self, d_in, d_out, npayloads, first, payload_bytes, payloads_per_key=0):
+        self._run(self._lib.cyaes_mgpu_decrypt_uniform, d_in, d_out, npayloads, first, payload_bytes,
+                  payloads_per_key)

@@ -18,11 +18,29 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_every_header_symbol():
     lib = ca.load_library()
     names = ca.header_functions()
-    assert len(names) >= 20
+    assert len(names) >= 40
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     # and the binding declares a signature for each of them
     assert sorted(ca._SIGS) == names
+
+
+def test_mgpu_library_exports_its_header():
+    lib = ca.load_mgpu_library()
+    names = ca.header_functions([ca.MGPU_HEADER])
+    assert names and all(hasattr(lib, n) for n in names)
+    assert sorted(ca._MGPU_SIGS) == names
+    assert ca.mgpu_shard(10, 3, 0) == (0, 3) and ca.mgpu_shard(10, 3, 2) == (6, 4)
+    assert ca.mgpu_shard(1024, 4, 1, align=256) == (256, 256)
+    covered = [ca.mgpu_shard(1000, 7, i, 16) for i in range(7)]
+    assert covered[0][0] == 0 and sum(c for _, c in covered) == 1000
+    assert all(a + c == b for (a, c), (b, _) in zip(covered, covered[1:]))
+
+
+def test_every_include_header_is_checked():
+    """Each include/*.h with a C-ABI is covered by one of the export checks above."""
+    hdrs = sorted(f for f in os.listdir(os.path.join(ROOT, "include")) if f.endswith(".h"))
+    assert hdrs == ["cyaes.h", "cyaes_batch.h", "cyaes_mgpu.h", "cyaes_relay.h"]
 
 
 def test_key_expand_matches_oracle(golden):
@@ -92,3 +110,10 @@ def test_cpp_dropin_builds_and_links():
     for sym in ("_ZN7cyclone8RijndaelC1EPKh", "_ZN7cyclone8Rijndael7encryptEPKhPhmS3_",
                 "_ZN7cyclone8Rijndael7decryptEPKhPhmS3_", "_ZN7cyclone8Rijndael9DefaultIVE"):
         assert sym in exported, sym
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-device path")
+def test_mgpu_without_device_fails_loudly():
+    with pytest.raises(ca.CyaesError) as e:
+        ca.MultiGpu([0])
+    assert e.value.status == ca.CYAES_ENODEV
