@@ -16,12 +16,14 @@ ORACLE   := oracle/liboracle.so
 CPPTEST  := $(BUILD)/test_rijndael
 
 KSRC     := cyclone_amd/csrc/cyaes_kernels.hip
+ASRC     := cyclone_amd/csrc/cyaes_adler.hip
 HSRC     := cyclone_amd/csrc/cyaes_runtime.cpp cyclone_amd/csrc/cyaes_tables.cpp cyclone_amd/csrc/cyr_rijndael.cpp \
             cyclone_amd/csrc/cyaes_relay.cpp cyclone_amd/csrc/cyaes_batcher.cpp
 HDRS     := include/cyaes.h include/cyaes_relay.h include/cyaes_batch.h include/cyclone_amd/cyr_rijndael.h cyclone_amd/csrc/cyaes_internal.h \
             cyclone_amd/csrc/cyaes_tables.h
 
 KOBJ     := $(BUILD)/cyaes_kernels.o
+AOBJ     := $(BUILD)/cyaes_adler.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
 .PHONY: all lib mgpu oracle cpptest microbench variant clean
@@ -37,10 +39,13 @@ $(BUILD):
 $(KOBJ): $(KSRC) $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(AOBJ): $(ASRC) include/cyaes_adler32.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/%.o: cyclone_amd/csrc/%.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
 
-$(LIB): $(KOBJ) $(HOBJ)
+$(LIB): $(KOBJ) $(AOBJ) $(HOBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
 
 # Single-process multi-GPU front end: separate library so libcyaes.so does not pull in RCCL.
@@ -62,10 +67,10 @@ $(BUILD)/microbench: tools/microbench.hip | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
 # A/B variants: make variant NAME=x DEFS="-DFOO=1" -> build/variants/x.so
-variant: $(HOBJ) | $(BUILD)
+variant: $(HOBJ) $(AOBJ) | $(BUILD)
 	mkdir -p $(BUILD)/variants
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(KSRC) -o $(BUILD)/variants/$(NAME).o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/$(NAME).so $(BUILD)/variants/$(NAME).o $(HOBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/$(NAME).so $(BUILD)/variants/$(NAME).o $(AOBJ) $(HOBJ)
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(MGPU) $(ORACLE)

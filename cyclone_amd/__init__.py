@@ -90,6 +90,9 @@ _SIGS = {
     "cyaes_relay_payloads": (ctypes.c_int64, [_vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint64, _vp, _vp]),
     "cyaes_relay_forward_id": (ctypes.c_int32, [_vp]),
     "cyaes_relay_forward_size": (ctypes.c_int32, [_vp]),
+    # include/cyaes_adler32.h
+    "cyaes_gpu_adler32_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+    "cyaes_gpu_adler32": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32, _u32p, _vp]),
     # include/cyaes_batch.h
     "cyaes_batcher_create": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "cyaes_batcher_destroy": (None, [_vp]),
@@ -108,7 +111,7 @@ _lib = None
 
 
 HEADERS = [os.path.join(os.path.dirname(_HERE), "include", h)
-           for h in ("cyaes.h", "cyaes_relay.h", "cyaes_batch.h")]
+           for h in ("cyaes.h", "cyaes_relay.h", "cyaes_batch.h", "cyaes_adler32.h")]
 MGPU_HEADER = os.path.join(os.path.dirname(_HERE), "include", "cyaes_mgpu.h")
 MGPU_LIB_PATH = os.path.join(_HERE, "libcyaes_mgpu.so")
 

@@ -327,3 +327,51 @@ int cyo_batch(int decrypt, const cyo_key* keys, uint32_t payloads_per_key, const
     free(th);
     return 0;
 }
+
+/* ---- Adler-32 (cyr_adler32.cpp:66-133), restated step for step ----------
+ * BASE 65521 (:12), NMAX 5552 (:13): sums of NMAX bytes fit 32 bits before a
+ * modulo.  Edge rules: NULL or len 0 -> INITIAL_ADLER (:72-73); len 1 uses
+ * two conditional subtractions (:80-87); len < 16 one subtraction for a and a
+ * modulo for sum2 (:90-98). */
+#define CYO_ADLER_BASE 65521u
+#define CYO_ADLER_NMAX 5552u
+
+uint32_t cyo_adler32(uint32_t adler, const uint8_t* buf, size_t len) {
+    if (buf == NULL || len == 0) return 1u;
+    uint32_t sum2 = (adler >> 16) & 0xffff;
+    adler &= 0xffff;
+    if (len == 1) {
+        adler += buf[0];
+        if (adler >= CYO_ADLER_BASE) adler -= CYO_ADLER_BASE;
+        sum2 += adler;
+        if (sum2 >= CYO_ADLER_BASE) sum2 -= CYO_ADLER_BASE;
+        return adler | (sum2 << 16);
+    }
+    if (len < 16) {
+        while (len--) {
+            adler += *buf++;
+            sum2 += adler;
+        }
+        if (adler >= CYO_ADLER_BASE) adler -= CYO_ADLER_BASE;
+        sum2 %= CYO_ADLER_BASE;
+        return adler | (sum2 << 16);
+    }
+    while (len >= CYO_ADLER_NMAX) { /* :105-114 */
+        len -= CYO_ADLER_NMAX;
+        for (unsigned n = 0; n < CYO_ADLER_NMAX; n++) {
+            adler += *buf++;
+            sum2 += adler;
+        }
+        adler %= CYO_ADLER_BASE;
+        sum2 %= CYO_ADLER_BASE;
+    }
+    if (len) { /* :117-129 */
+        while (len--) {
+            adler += *buf++;
+            sum2 += adler;
+        }
+        adler %= CYO_ADLER_BASE;
+        sum2 %= CYO_ADLER_BASE;
+    }
+    return adler | (sum2 << 16);
+}

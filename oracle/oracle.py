@@ -157,3 +157,14 @@ def digest(buf):
     with np.errstate(over="ignore"):
         s = np.add.reduce(h, dtype=np.uint64) if h.size else np.uint64(0)
     return int(x), int(s)
+
+
+def adler32(adler, data):
+    """cyclone::adler32 (cyr_adler32.cpp:66-133); data None => the NULL-buffer rule."""
+    f = lib().cyo_adler32
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+    if data is None:
+        return f(adler, None, 0)
+    arr = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    return f(adler, arr.ctypes.data if arr.size else None, arr.size)

@@ -6,7 +6,8 @@ nothing is compiled, imported or executed).  Writes data, not source:
 
   ref_kat.json / ref_kat.txt  -- the Rijndael known-answer vector of
       test/unit/cyt_unit_crypt.cpp:177-186 (key, plaintext, ciphertext,
-      iv_check), as hex.
+      iv_check), as hex; and (ref_kat.json "adler32") the Adler-32 known
+      answers of cyt_unit_crypt.cpp:18-50.
   ref_tables.json             -- SHA-256 of each static table of
       source/cyCrypt/crypt/cyr_rijndael.cpp:25-501 (S, Si, T1..T8, U1..U4,
       rcon), serialised as little-endian u8/u32 arrays, plus DefaultIV
@@ -57,6 +58,24 @@ def kat():
             "random_roundtrip_bytes": 128}
 
 
+def adler_kat():
+    """Adler-32 known answers of test/unit/cyt_unit_crypt.cpp:18-50 (strings,
+    the 64-byte data_buf, its split point) as data."""
+    src = open(os.path.join(REF, "test/unit/cyt_unit_crypt.cpp"), encoding="utf-8-sig").read()
+    body = src[src.index('TEST_CASE("Crypto algorithm(Adler32) basic test"'):]
+    body = body[:body.index("TEST_CASE", 10)]
+    strings = re.findall(r'const char\* \w+ = "(.*?)";\s*(?:uint32_t )?adler = adler32\(INITIAL_ADLER.*?\);\s*'
+                         r'REQUIRE_EQ\((0x[0-9a-fA-F]+)ul, adler\);', body, re.S)
+    data = bytes(_ints(re.search(r"data_buf\[\]\s*=\s*\{(.*?)\};", body, re.S).group(1)))
+    expect = int(re.search(r"REQUIRE_EQ\((0x[0-9a-fA-F]+)ul, adler1\)", body).group(1), 16)
+    first = int(re.search(r"size_t first = (\d+);", body).group(1))
+    assert len(strings) == 2 and len(data) == 64
+    return {"source": "test/unit/cyt_unit_crypt.cpp:18-50",
+            "strings": [{"text": t, "adler": int(a, 16)} for t, a in strings],
+            "data_buf": data.hex(), "data_adler": expect, "split": first,
+            "null_or_empty": 1, "random_cases": 100, "random_cap": 257}
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not present; fixtures are committed, nothing to do")
@@ -66,6 +85,9 @@ def main():
     with open(os.path.join(HERE, "ref_kat.txt"), "w") as f:
         for name in ["key", "plaintext", "ciphertext", "iv_check"]:
             f.write("%s=%s\n" % (name, k[name]))
+    k["adler32"] = adler_kat()
+    with open(os.path.join(HERE, "ref_kat.json"), "w") as f:
+        json.dump(k, f, indent=1)
     t = tables()
     t["source"] = "source/cyCrypt/crypt/cyr_rijndael.cpp:25-504"
     with open(os.path.join(HERE, "ref_tables.json"), "w") as f:

@@ -146,3 +146,37 @@ def test_digest_definition():
     hs = [int(oracle._splitmix64(np.uint64(v) ^ oracle._splitmix64(np.uint64(i)))) for i, v in enumerate([1, 2, 3])]
     assert x == hs[0] ^ hs[1] ^ hs[2] and s == sum(hs) % (1 << 64)
     assert struct.calcsize("<Q") == 8
+
+
+# ---- Adler-32 (cyr_adler32.cpp:66-133) -------------------------------------
+def test_adler32_oracle_reference_kat(golden):
+    """The reference's own known answers, test/unit/cyt_unit_crypt.cpp:18-50."""
+    k = golden["kat"]["adler32"]
+    assert oracle.adler32(0, None) == k["null_or_empty"] == 1
+    assert oracle.adler32(0xFFFFFFFF, None) == 1
+    for s in k["strings"]:
+        assert oracle.adler32(1, s["text"].encode()) == s["adler"]
+    data = bytes.fromhex(k["data_buf"])
+    assert oracle.adler32(1, data) == k["data_adler"]
+    first = k["split"]
+    assert oracle.adler32(oracle.adler32(1, data[:first]), data[first:]) == k["data_adler"]
+
+
+def test_adler32_oracle_random_split_and_zlib():
+    """cyt_unit_crypt.cpp:54-78 (random split property) and, independently,
+    zlib's adler32 (same algorithm) for every length class of the reference's
+    code paths (1, <16, NMAX blocks)."""
+    import zlib
+    rng = random.Random(31)
+    for _ in range(100):
+        size = 257 - rng.randrange(32)
+        buf = bytes(rng.randrange(256) for _ in range(size))
+        cut = rng.randrange(size - 1) + 1
+        assert oracle.adler32(oracle.adler32(1, buf[:cut]), buf[cut:]) == oracle.adler32(1, buf)
+    for n in [1, 2, 15, 16, 17, 5551, 5552, 5553, 11104, 20000]:
+        buf = bytes(rng.randrange(256) for _ in range(n))
+        start = zlib.adler32(bytes(rng.randrange(256) for _ in range(7)))
+        assert oracle.adler32(1, buf) == zlib.adler32(buf)
+        assert oracle.adler32(start, buf) == zlib.adler32(buf, start)
+    # the reference's own rule differs from zlib for len == 0
+    assert oracle.adler32(0xdeadbeef, b"") == 1 and zlib.adler32(b"", 0xdeadbeef) == 0xdeadbeef
