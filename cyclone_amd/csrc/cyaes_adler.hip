@@ -83,10 +83,25 @@ __device__ __forceinline__ Part slice(const uint8_t* buf, uint64_t n, uint64_t l
     // im = (h + 16 * j) mod kBase, advanced by 16 * nl per step
     const uint32_t step = (uint32_t)((16 * nl) % kBase);
     uint32_t im = (uint32_t)((h + 16 * l) % kBase);
-    for (uint64_t j = l; j < nvec; j += nl) {
-        add_vec(p, v[j], im);
+    auto adv = [&]() {
         im += step;
         if (im >= kBase) im -= kBase;
+    };
+    uint64_t j = l;
+    for (; j + 3 * nl < nvec; j += 4 * nl) {  // four independent loads in flight per lane
+        const uint4 a = v[j], b = v[j + nl], c = v[j + 2 * nl], d = v[j + 3 * nl];
+        add_vec(p, a, im);
+        adv();
+        add_vec(p, b, im);
+        adv();
+        add_vec(p, c, im);
+        adv();
+        add_vec(p, d, im);
+        adv();
+    }
+    for (; j < nvec; j += nl) {
+        add_vec(p, v[j], im);
+        adv();
     }
     p.s %= kBase;
     p.t %= kBase;
