@@ -28,6 +28,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "AES encrypt+decrypt GiB/s device-resident (64 KiB payloads); % HBM roofline @1/2/4/8 GPU"
+LOOKUPS_PER_BLOCK = 160      # 9 x 16 T-table + 16 S-box lookups (cyr_rijndael.cpp:659-704)
+LDS_LANES_PER_CLK_CU = 32    # ds_read_b32: 2 x 32-lane groups, 1 cycle each (MI355X_MICROARCH.md, LDS)
+NUM_CUS = 256
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 PLAINTEXT_SEED = 0x5EEDC1C1
 CONFIGS = {
@@ -220,8 +223,18 @@ def main():
         return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4)}
 
-    kern = {"encrypt": dict(roof(enc_ms), avg_ms=round(enc_ms, 4)),
-            "decrypt": dict(roof(dec_ms), avg_ms=round(dec_ms, 4))}
+    def lds(ms):
+        # The binding on-chip resource: 160 conflict-free ds_read_b32
+        # lookups per 16-B block; nominal LDS rate 32 lanes/clk/CU (2 cycles per wave64
+        # ds_read_b32), here priced at the 2.4 GHz peak shader clock.  In-kernel clock
+        # probes (tools/ab.py + CYAES_CLOCK_PROBE) show ~1.9 GHz under this load.
+        look = LOOKUPS_PER_BLOCK * (nbytes / 16) / (ms / 1e3)
+        peak = LDS_LANES_PER_CLK_CU * NUM_CUS * 2.4e9
+        return {"lookups_per_s": float("%.4g" % look), "peak_at_2p4ghz": float("%.4g" % peak),
+                "frac": round(look / peak, 4)}
+
+    kern = {"encrypt": dict(roof(enc_ms), avg_ms=round(enc_ms, 4), lds=lds(enc_ms)),
+            "decrypt": dict(roof(dec_ms), avg_ms=round(dec_ms, 4), lds=lds(dec_ms))}
     dom = "encrypt" if enc_ms >= dec_ms else "decrypt"
     roofline = dict(roof(enc_ms if dom == "encrypt" else dec_ms), kernel=dom, traffic=None)
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
