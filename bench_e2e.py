@@ -2,12 +2,14 @@
 """bench_e2e.py -- host-to-host AES-128-CBC throughput (PCIe-inclusive).
 
 The relay path starts and ends in host memory (socket buffers, SURVEY.md
-§3.1-3.2).  This measures the rate including hipMemcpyAsync over pinned
-staging buffers: the batch lives in pinned host memory; chunks of
-`--chunk-mib` are copied H2D, encrypted (or decrypted) on the GPU and copied
-back D2H, with `--streams` streams in flight so copies in both directions
-overlap the kernels.  Reported per direction and as the encrypt+decrypt
-figure of the headline metric, 2N / (t_enc + t_dec).  Not the bench.py value.
+§3.1-3.2).  This measures cyaes_gpu_{en,de}crypt_host (include/cyaes.h): the
+batch lives in host memory; the library streams chunks H2D -> kernel -> D2H
+on three streams (upload / compute / download) over a ring of device slots,
+so both copy directions overlap each other and the kernels.  Host buffers are
+pinned (`--host pinned`, hipHostMalloc via torch) or pageable (`--host
+pageable`, numpy; the library registers them for the call).  Reported per
+direction and as the encrypt+decrypt figure of the headline metric,
+2N / (t_enc + t_dec).  Not the bench.py value.
 """
 import argparse
 import json
@@ -21,10 +23,10 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--payloads", type=int, default=65536)
+    ap.add_argument("--payloads", type=int, default=131072)
     ap.add_argument("--payload-bytes", type=int, default=65536)
     ap.add_argument("--chunk-mib", type=int, default=256)
-    ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--host", default="pinned", choices=["pinned", "pageable"])
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
 
@@ -35,45 +37,34 @@ def main():
 
     pb, n = args.payload_bytes, args.payloads
     nbytes = n * pb
-    per_chunk = max(1, (args.chunk_mib << 20) // pb)
-    chunk = per_chunk * pb
+    chunk = args.chunk_mib << 20
     ctx = ca.GpuContext(0)
     ctx.set_keys(bytes(range(16)))
-    # pinned host batch (the "socket buffers" after gather) + staging-free device ring
-    h_pt = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    h_ct = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    h_rt = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    d_tmp = torch.empty(nbytes if nbytes < chunk else chunk, dtype=torch.uint8, device="cuda")
-    ctx.fill_synthetic(d_tmp, 0, min(n, per_chunk), pb, 0x5EEDC1C1)
-    for c0 in range(0, n, per_chunk):  # synthetic plaintext, generated on device chunk by chunk
-        cn = min(per_chunk, n - c0)
+    pinned = args.host == "pinned"
+
+    def hbuf():
+        return torch.empty(nbytes, dtype=torch.uint8, pin_memory=pinned)
+    h_pt, h_ct, h_rt = hbuf(), hbuf(), hbuf()
+    # synthetic plaintext, generated on the device piece by piece
+    per = max(1, (1 << 30) // pb)
+    d_tmp = torch.empty(min(n, per) * pb, dtype=torch.uint8, device="cuda")
+    for c0 in range(0, n, per):
+        cn = min(per, n - c0)
         ctx.fill_synthetic(d_tmp, c0, cn, pb, 0x5EEDC1C1)
         h_pt[c0 * pb:(c0 + cn) * pb].copy_(d_tmp[:cn * pb])
     torch.cuda.synchronize()
     del d_tmp
-    streams = [torch.cuda.Stream() for _ in range(args.streams)]
-    din = [torch.empty(chunk, dtype=torch.uint8, device="cuda") for _ in streams]
-    dout = [torch.empty(chunk, dtype=torch.uint8, device="cuda") for _ in streams]
 
-    def run(decrypt, src, dst):
-        torch.cuda.synchronize()
+    def run(fn, src, dst):
         t0 = time.perf_counter()
-        for i, c0 in enumerate(range(0, n, per_chunk)):
-            k = i % len(streams)
-            s = streams[k]
-            cn = min(per_chunk, n - c0)
-            with torch.cuda.stream(s):
-                din[k][:cn * pb].copy_(src[c0 * pb:(c0 + cn) * pb], non_blocking=True)
-                fn = ctx.decrypt_uniform if decrypt else ctx.encrypt_uniform
-                fn(din[k], dout[k], cn, pb, stream=s.cuda_stream)
-                dst[c0 * pb:(c0 + cn) * pb].copy_(dout[k][:cn * pb], non_blocking=True)
-        torch.cuda.synchronize()
+        fn(src.data_ptr(), dst.data_ptr(), n, pb, chunk_bytes=chunk)
         return time.perf_counter() - t0
 
+    run(ctx.encrypt_host, h_pt, h_ct)  # first call sizes the device slot ring
     best_e = best_d = 1e30
     for _ in range(args.reps):
-        best_e = min(best_e, run(False, h_pt, h_ct))
-        best_d = min(best_d, run(True, h_ct, h_rt))
+        best_e = min(best_e, run(ctx.encrypt_host, h_pt, h_ct))
+        best_d = min(best_d, run(ctx.decrypt_host, h_ct, h_rt))
     ok = bool(torch.equal(h_rt, h_pt))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -82,8 +73,8 @@ def main():
     ok = ok and bool(np.array_equal(h_ct[:sample * pb].numpy(), want))
     gib = float(1 << 30)
     print(json.dumps({
-        "metric": "AES-128-CBC host-to-host GiB/s over pinned staging (PCIe-inclusive)",
-        "payloads": n, "payload_bytes": pb, "chunk_mib": chunk >> 20, "streams": args.streams,
+        "metric": "AES-128-CBC host-to-host GiB/s, cyaes_gpu_{en,de}crypt_host (PCIe-inclusive)",
+        "payloads": n, "payload_bytes": pb, "chunk_mib": args.chunk_mib, "host_memory": args.host,
         "encrypt_gibs": round(nbytes / best_e / gib, 2), "decrypt_gibs": round(nbytes / best_d / gib, 2),
         "enc_plus_dec_gibs": round(2 * nbytes / (best_e + best_d) / gib, 2),
         "h2d_plus_d2h_bytes_per_direction": 2 * nbytes, "parity": "bit-exact" if ok else "MISMATCH",

@@ -75,6 +75,10 @@ _SIGS = {
     "cyaes_gpu_decrypt_ragged": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32,
                                                 _vp, _vp, _vp]),
     "cyaes_gpu_check": (ctypes.c_int, [_vp]),
+    "cyaes_gpu_encrypt_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                              ctypes.c_uint64]),
+    "cyaes_gpu_decrypt_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                              ctypes.c_uint64]),
     "cyaes_gpu_fill_synthetic": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                                 ctypes.c_uint64, _vp]),
     "cyaes_gpu_digest": (ctypes.c_int, [_vp, ctypes.c_uint64, _u64p, _vp]),
@@ -324,6 +328,15 @@ class GpuContext:
         _check(self._lib.cyaes_gpu_decrypt_ragged(self._h, _p(d_in), _p(d_out), _p(offsets), _p(nbytes), npayloads,
                                                   _p(key_idx), payloads_per_key, _p(iv_in), _p(iv_out),
                                                   _p(stream)), "decrypt_ragged")
+
+    def encrypt_host(self, h_in, h_out, npayloads, payload_bytes, payloads_per_key=0, chunk_bytes=0):
+        """Host-resident batch (host addresses or CPU tensors), PCIe-inclusive; synchronous."""
+        _check(self._lib.cyaes_gpu_encrypt_host(self._h, _p(h_in), _p(h_out), npayloads, payload_bytes,
+                                                payloads_per_key, chunk_bytes), "encrypt_host")
+
+    def decrypt_host(self, h_in, h_out, npayloads, payload_bytes, payloads_per_key=0, chunk_bytes=0):
+        _check(self._lib.cyaes_gpu_decrypt_host(self._h, _p(h_in), _p(h_out), npayloads, payload_bytes,
+                                                payloads_per_key, chunk_bytes), "decrypt_host")
 
     def check(self):
         """CYAES_OK, or CYAES_ERANGE if a batch clamped a key index (no raise)."""

@@ -521,7 +521,7 @@ __device__ __forceinline__ void flat_load(const DecArgs& a, uint32_t lane, uint6
 template <bool KEYED, bool BIG, bool FULL>
 __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, uint32_t lo, uint32_t lane,
                                            uint64_t base, uint64_t end, FlatPos ps, uint4 carry,
-                                           const uint32_t (&dk0)[44], const uint4 (&c)[kDecRows],
+                                           uint32_t (&dk0)[44], uint32_t& dk_id, const uint4 (&c)[kDecRows],
                                            uint4 (&pv)[kDecRows]) {
     constexpr int R = kDecRows;
     uint4* out = reinterpret_cast<uint4*>(a.out);
@@ -588,26 +588,50 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
         dec_cbc<R>(lds, lo, dk0, c, d);  // all R rows per LDS round trip (A/B: ~1% over 2 rows)
 #endif
     } else {
+        uint32_t kid[R];
+        bool valid[R];
 #pragma unroll
         for (int k = 0; k < R; k++) {
             uint32_t r;
             uint64_t p;
             flat_position<BIG>(a, ps, lane, k, r, p);
-            const bool valid = FULL || base + 64 * k + lane < end;
-            const uint32_t kid = key_index(a.keys, p, valid, a.status);
-            bool pending = valid;
-            while (true) {  // waterfall over the distinct keys of this row
-                const uint64_t m = __ballot(pending);
-                if (m == 0) break;
-                const uint32_t ku = __builtin_amdgcn_readlane(kid, __builtin_ctzll(m));
-                if (pending && kid == ku) {
-                    pending = false;
-                    uint32_t dk[44];
-                    load_sched(a.keys.table + (uint64_t)ku * kSchedWords + 44, dk);
-                    const uint4 cc[1] = {c[k]};
-                    uint4 dd[1] = {d[k]};
-                    dec_cbc<1>(lds, lo, dk, cc, dd);
-                    d[k] = dd[0];
+            valid[k] = FULL || base + 64 * k + lane < end;
+            kid[k] = key_index(a.keys, p, valid[k], a.status);
+        }
+        // Sessions are contiguous runs of payloads (config D: 256 x 92 blocks),
+        // so nearly every full step has one key: decrypt all R rows together
+        // under it (R-way ILP), as the unkeyed path does.  Otherwise fall back
+        // to a per-row waterfall over the keys present.
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(kid[0]);
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < R; k++) same = same && kid[k] == k0;
+        const bool uniform = FULL && __ballot(!same) == 0;
+        if (uniform) {
+            // dk0 keeps the last session's schedule (SGPRs) across steps: a
+            // session spans ~92 steps in config D
+            if (k0 != dk_id) {
+                load_sched(a.keys.table + (uint64_t)k0 * kSchedWords + 44, dk0);
+                dk_id = k0;
+            }
+            dec_cbc<R>(lds, lo, dk0, c, d);
+        } else {
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                bool pending = valid[k];
+                while (true) {  // waterfall over the distinct keys of this row
+                    const uint64_t m = __ballot(pending);
+                    if (m == 0) break;
+                    const uint32_t ku = __builtin_amdgcn_readlane(kid[k], __builtin_ctzll(m));
+                    if (pending && kid[k] == ku) {
+                        pending = false;
+                        uint32_t dk[44];
+                        load_sched(a.keys.table + (uint64_t)ku * kSchedWords + 44, dk);
+                        const uint4 cc[1] = {c[k]};
+                        uint4 dd[1] = {d[k]};
+                        dec_cbc<1>(lds, lo, dk, cc, dd);
+                        d[k] = dd[0];
+                    }
                 }
             }
         }
@@ -648,20 +672,22 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     uint4 carry = make_uint4(0, 0, 0, 0);  // C[base-1]
     if (ps.bpos != 0) carry = a.boundary ? a.boundary[wave] : reinterpret_cast<const uint4*>(a.in)[begin - 1];
     uint32_t dk0[44];
+    uint32_t dk_id = 0;  // KEYED: session whose schedule dk0 holds (~0u: none yet)
     if (!KEYED) load_sched(a.keys.table + 44, dk0);
+    else dk_id = ~0u;
     uint64_t base = begin;
     uint4 c[R], pv[R];
     if (base + 64 * R <= end) flat_load<true>(a, lane, base, end, c, pv);
     for (; base + 64 * R <= end; base += 64 * R) {
 #if !CYAES_DEC_PREFETCH  // A/B (tools/ab.py): prefetching the next step costs ~1% here
-        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0, c, pv);
+        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv);
         if (base + 128 * R <= end) flat_load<true>(a, lane, base + 64 * R, end, c, pv);
 #else
         // Issue the next step's loads before this step's rounds.
         uint4 cn[R], pvn[R];
         const bool more = base + 128 * R <= end;
         if (more) flat_load<true>(a, lane, base + 64 * R, end, cn, pvn);
-        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0, c, pv);
+        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv);
         if (more) {
 #pragma unroll
             for (int k = 0; k < R; k++) { c[k] = cn[k]; pv[k] = pvn[k]; }
@@ -674,7 +700,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     }
     if (base < end) {
         flat_load<false>(a, lane, base, end, c, pv);
-        flat_step<KEYED, BIG, false>(a, lds, lo, lane, base, end, ps, carry, dk0, c, pv);
+        flat_step<KEYED, BIG, false>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv);
     }
 }
 

@@ -28,6 +28,7 @@ struct cyaes_gpu {
     uint32_t* d_status = nullptr;
     unsigned long long* d_digest = nullptr;
     hipStream_t last_stream = nullptr;
+    struct HostPipe* pipe = nullptr;  // cyaes_gpu_{en,de}crypt_host, created on first use
 };
 
 namespace {
@@ -220,6 +221,8 @@ bool ragged_args_ok(const cyaes_gpu* ctx, const uint8_t* in, const uint8_t* out,
 
 }  // namespace
 
+static void destroy_pipe(HostPipe* p);
+
 int cyaes::ragged_batch(cyaes_gpu* ctx, bool decrypt, const uint32_t* d_table, uint32_t table_keys,
                         const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
                         uint64_t npayloads, const uint32_t* key_idx, hipStream_t stream) {
@@ -300,6 +303,7 @@ void cyaes_gpu_destroy(cyaes_gpu* ctx) {
     (void)hipFree(ctx->d_iv_scratch);
     (void)hipFree(ctx->d_status);
     (void)hipFree(ctx->d_digest);
+    destroy_pipe(ctx->pipe);
     delete ctx;
 }
 
@@ -594,6 +598,159 @@ int cyaes_cbc_encrypt(const cyaes_key* key, const uint8_t* in, uint8_t* out, siz
 
 int cyaes_cbc_decrypt(const cyaes_key* key, const uint8_t* in, uint8_t* out, size_t size, uint8_t* iv) {
     return dropin_run(true, key, in, out, size, iv);
+}
+
+}  // extern "C"
+
+// ---- host-resident batches streamed through the device --------------------
+// The relay path starts and ends in host memory.  Three
+// streams -- upload, compute, download -- and a ring of kSlots device slot
+// pairs: chunk i uses slot i % kSlots; its upload waits for the kernel of
+// chunk i - kSlots (slot input free), its kernel for its upload and for the
+// download of chunk i - kSlots (slot output free).  Both copy directions then
+// run back to back and overlap each other and the kernels.
+struct HostPipe {
+    static constexpr int kSlots = 3;
+    int device = 0;
+    hipStream_t up = nullptr, comp = nullptr, down = nullptr;
+    hipEvent_t ev_up[kSlots] = {}, ev_comp[kSlots] = {}, ev_down[kSlots] = {};
+    uint8_t* d_in[kSlots] = {};
+    uint8_t* d_out[kSlots] = {};
+    uint64_t cap = 0;
+};
+
+static void destroy_pipe(HostPipe* p) {
+    if (!p) return;
+    for (int i = 0; i < HostPipe::kSlots; i++) {
+        (void)hipFree(p->d_in[i]);
+        (void)hipFree(p->d_out[i]);
+        if (p->ev_up[i]) (void)hipEventDestroy(p->ev_up[i]);
+        if (p->ev_comp[i]) (void)hipEventDestroy(p->ev_comp[i]);
+        if (p->ev_down[i]) (void)hipEventDestroy(p->ev_down[i]);
+    }
+    for (hipStream_t s : {p->up, p->comp, p->down})
+        if (s) (void)hipStreamDestroy(s);
+    delete p;
+}
+
+namespace {
+
+int pipe_ready(cyaes_gpu* ctx, uint64_t slot_bytes) {
+    if (!ctx->pipe) {
+        HostPipe* p = new HostPipe();
+        p->device = ctx->device;
+        ctx->pipe = p;
+        for (hipStream_t* s : {&p->up, &p->comp, &p->down}) CY_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+        for (int i = 0; i < HostPipe::kSlots; i++) {
+            CY_TRY(hipEventCreateWithFlags(&p->ev_up[i], hipEventDisableTiming));
+            CY_TRY(hipEventCreateWithFlags(&p->ev_comp[i], hipEventDisableTiming));
+            CY_TRY(hipEventCreateWithFlags(&p->ev_down[i], hipEventDisableTiming));
+        }
+    }
+    HostPipe* p = ctx->pipe;
+    if (p->cap < slot_bytes) {
+        CY_TRY(hipDeviceSynchronize());
+        for (int i = 0; i < HostPipe::kSlots; i++) {
+            (void)hipFree(p->d_in[i]);
+            (void)hipFree(p->d_out[i]);
+            p->d_in[i] = p->d_out[i] = nullptr;
+        }
+        p->cap = 0;
+        for (int i = 0; i < HostPipe::kSlots; i++) {
+            CY_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_in[i]), slot_bytes));
+            CY_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_out[i]), slot_bytes));
+        }
+        p->cap = slot_bytes;
+    }
+    return CYAES_OK;
+}
+
+bool host_pinned(const void* ptr) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+// Pins a pageable host range for the duration of a call (DMA straight from
+// and to the caller's memory instead of the runtime's bounce buffers).  A
+// range that cannot be registered is left pageable; the copies still work.
+struct HostPin {
+    void* ptr = nullptr;
+    explicit HostPin(const void* p, uint64_t bytes) {
+        if (host_pinned(p)) return;
+        if (hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) == hipSuccess)
+            ptr = const_cast<void*>(p);
+        else
+            (void)hipGetLastError();
+    }
+    ~HostPin() {
+        if (ptr) (void)hipHostUnregister(ptr);
+    }
+};
+
+int host_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* h_in, uint8_t* h_out, uint64_t npayloads,
+               uint32_t payload_bytes, uint32_t ppk, uint64_t chunk_bytes) {
+    if (!ctx || !h_in || !h_out || payload_bytes % 16) return CYAES_EINVAL;
+    if (npayloads == 0 || payload_bytes == 0) return CYAES_OK;
+    if (ctx->nkeys == 0) return CYAES_ERANGE;
+    if (ppk && (npayloads - 1) / ppk >= ctx->nkeys) return CYAES_ERANGE;
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return CYAES_EDEVICE;
+    if (chunk_bytes == 0) chunk_bytes = 256ull << 20;
+    // Chunks hold whole payloads, and whole sessions when keys are per session,
+    // so chunk c starts at session c0 / ppk and runs under that table slice.
+    uint64_t cp = std::max<uint64_t>(1, chunk_bytes / payload_bytes);
+    if (ppk) cp = std::max<uint64_t>(ppk, cp / ppk * ppk);
+    cp = std::min(cp, npayloads);
+    const uint64_t total = npayloads * payload_bytes;
+    int st = pipe_ready(ctx, cp * payload_bytes);
+    if (st) return st;
+    HostPin pin_in(h_in, total);
+    HostPin pin_out(h_out, (h_out == h_in) ? 0 : total);
+    HostPipe* p = ctx->pipe;
+    uint64_t i = 0;
+    for (uint64_t c0 = 0; c0 < npayloads; c0 += cp, i++) {
+        const int s = (int)(i % HostPipe::kSlots);
+        const uint64_t n = std::min(cp, npayloads - c0);
+        const uint64_t off = c0 * payload_bytes, bytes = n * payload_bytes;
+        if (i >= (uint64_t)HostPipe::kSlots) CY_TRY(hipStreamWaitEvent(p->up, p->ev_comp[s], 0));
+        CY_TRY(hipMemcpyAsync(p->d_in[s], h_in + off, bytes, hipMemcpyHostToDevice, p->up));
+        CY_TRY(hipEventRecord(p->ev_up[s], p->up));
+        CY_TRY(hipStreamWaitEvent(p->comp, p->ev_up[s], 0));
+        if (i >= (uint64_t)HostPipe::kSlots) CY_TRY(hipStreamWaitEvent(p->comp, p->ev_down[s], 0));
+        const uint64_t k0 = ppk ? c0 / ppk : 0;
+        const uint32_t* table = ctx->d_keys + k0 * kSchedWords;
+        const uint32_t tkeys = ctx->nkeys - (uint32_t)k0;
+        st = decrypt ? decrypt_uniform(ctx, p->d_in[s], p->d_out[s], n, payload_bytes, nullptr, ppk, nullptr, nullptr,
+                                       p->comp, table, tkeys)
+                     : encrypt_common(ctx, p->d_in[s], p->d_out[s], nullptr, nullptr, n, payload_bytes, nullptr, ppk,
+                                      nullptr, nullptr, p->comp, table, tkeys);
+        if (st) return st;
+        CY_TRY(hipEventRecord(p->ev_comp[s], p->comp));
+        CY_TRY(hipStreamWaitEvent(p->down, p->ev_comp[s], 0));
+        CY_TRY(hipMemcpyAsync(h_out + off, p->d_out[s], bytes, hipMemcpyDeviceToHost, p->down));
+        CY_TRY(hipEventRecord(p->ev_down[s], p->down));
+    }
+    CY_TRY(hipStreamSynchronize(p->down));
+    ctx->last_stream = p->down;
+    return CYAES_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cyaes_gpu_encrypt_host(cyaes_gpu* ctx, const uint8_t* h_in, uint8_t* h_out, uint64_t npayloads,
+                           uint32_t payload_bytes, uint32_t payloads_per_key, uint64_t chunk_bytes) {
+    return host_batch(ctx, false, h_in, h_out, npayloads, payload_bytes, payloads_per_key, chunk_bytes);
+}
+
+int cyaes_gpu_decrypt_host(cyaes_gpu* ctx, const uint8_t* h_in, uint8_t* h_out, uint64_t npayloads,
+                           uint32_t payload_bytes, uint32_t payloads_per_key, uint64_t chunk_bytes) {
+    return host_batch(ctx, true, h_in, h_out, npayloads, payload_bytes, payloads_per_key, chunk_bytes);
 }
 
 }  // extern "C"

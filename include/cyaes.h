@@ -131,6 +131,22 @@ int cyaes_gpu_cbc_decrypt_batch(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_
                                 const uint32_t* d_nbytes, const uint32_t* d_key_idx, const uint8_t* d_iv,
                                 uint32_t npayloads, void* stream);
 
+/* ---- Host-resident uniform batches (PCIe-inclusive) ----------------------
+ * The relay path starts and ends in host memory (socket buffers).  These
+ * process npayloads uniform payloads that live in HOST memory: chunks of
+ * chunk_bytes (0 = 256 MiB; rounded to whole payloads, and to whole sessions
+ * when payloads_per_key != 0) are copied H2D, en/decrypted and copied D2H on
+ * three streams (upload, compute, download) over a ring of three device slot
+ * pairs, so both copy directions and the kernels overlap.  h_in / h_out may be
+ * pinned (hipHostMalloc, hipHostRegister) or pageable; pageable ranges are
+ * registered for the duration of the call.  h_in == h_out is allowed.  Every
+ * payload is a chain from DefaultIV; key of payload p = payloads_per_key ?
+ * p / payloads_per_key : 0.  Synchronous: returns when h_out is complete. */
+int cyaes_gpu_encrypt_host(cyaes_gpu* ctx, const uint8_t* h_in, uint8_t* h_out, uint64_t npayloads,
+                           uint32_t payload_bytes, uint32_t payloads_per_key, uint64_t chunk_bytes);
+int cyaes_gpu_decrypt_host(cyaes_gpu* ctx, const uint8_t* h_in, uint8_t* h_out, uint64_t npayloads,
+                           uint32_t payload_bytes, uint32_t payloads_per_key, uint64_t chunk_bytes);
+
 /* Synchronises the context's last-used stream and returns CYAES_ERANGE if a
  * batch since the previous check saw an out-of-range key index (sticky flag
  * is then cleared), CYAES_EDEVICE on an asynchronous HIP error, else CYAES_OK. */

@@ -148,6 +148,75 @@ def test_session_keys_payloads_per_key(torch, ctx):
     c.close()
 
 
+@pytest.mark.parametrize("pb,ppk,nk", [(1472, 256, 6), (65536, 3, 4), (208, 1000, 3)])
+def test_session_keys_uniform_steps(torch, pb, ppk, nk):
+    """Sessions spanning many decrypt steps (config D: 256 x 1472 B per key): the
+    one-key-per-step fast path, and the steps that straddle a session boundary."""
+    n = nk * ppk - 5  # last session partial
+    keys = [oracle.session_key(100 + s) for s in range(nk)]
+    c = ca.GpuContext(0)
+    c.set_keys(b"".join(keys))
+    pt = oracle.synthetic(11, n, pb)
+    want = oracle.batch(False, keys, ppk, pt, pb, nthreads=16)
+    d_pt, d_ct, d_rt = dev(torch, pt), empty(torch, pt.size), empty(torch, pt.size)
+    c.encrypt_uniform(d_pt, d_ct, n, pb, payloads_per_key=ppk)
+    assert np.array_equal(host(d_ct), want)
+    c.decrypt_uniform(d_ct, d_rt, n, pb, payloads_per_key=ppk)
+    assert np.array_equal(host(d_rt), pt)
+    c.decrypt_uniform(d_ct, d_ct, n, pb, payloads_per_key=ppk)  # in place
+    assert np.array_equal(host(d_ct), pt)
+    assert c.check() == ca.CYAES_OK
+    c.close()
+
+
+# ------------------------------------------------- host-resident batches --
+@pytest.mark.parametrize("pinned", [True, False])
+def test_host_batches_streamed(torch, pinned):
+    """cyaes_gpu_{en,de}crypt_host: host memory in and out, several chunks per
+    call (3-slot ring wraps), per-session keys, pinned and pageable buffers."""
+    nk, ppk, pb = 9, 40, 1472
+    n = nk * ppk - 3
+    keys = [oracle.session_key(s) for s in range(nk)]
+    c = ca.GpuContext(0)
+    c.set_keys(b"".join(keys))
+    pt = oracle.synthetic(5, n, pb)
+    want = oracle.batch(False, keys, ppk, pt, pb, nthreads=16)
+
+    def buf(a=None):
+        t = torch.empty(pt.size, dtype=torch.uint8, pin_memory=pinned)
+        if a is not None:
+            t.copy_(torch.from_numpy(a))
+        return t
+    h_pt, h_ct, h_rt = buf(pt), buf(), buf()
+    chunk = 2 * ppk * pb  # 2 sessions per chunk -> 5 chunks
+    c.encrypt_host(h_pt, h_ct, n, pb, payloads_per_key=ppk, chunk_bytes=chunk)
+    assert np.array_equal(h_ct.numpy(), want)
+    c.decrypt_host(h_ct, h_rt, n, pb, payloads_per_key=ppk, chunk_bytes=chunk)
+    assert np.array_equal(h_rt.numpy(), pt)
+    c.decrypt_host(h_ct, h_ct, n, pb, payloads_per_key=ppk, chunk_bytes=1)  # in place, one session per chunk
+    assert np.array_equal(h_ct.numpy(), pt)
+    c.encrypt_host(h_pt, h_ct, n, pb, payloads_per_key=ppk)  # default chunk: one
+    assert np.array_equal(h_ct.numpy(), want)
+    with pytest.raises(ca.CyaesError):  # (n-1)/ppk >= nkeys
+        c.encrypt_host(h_pt, h_ct, n, pb, payloads_per_key=ppk // 4)
+    with pytest.raises(ca.CyaesError):
+        c.encrypt_host(h_pt, h_ct, n, pb + 8)
+    c.close()
+
+
+def test_host_batch_single_key_large(torch, ctx):
+    """One key, 64 KiB payloads, 4 chunks of 4 MiB."""
+    n, pb = 256, 65536
+    pt = oracle.synthetic(0, n, pb)
+    want = oracle.batch(False, [K0], 0, pt, pb, nthreads=16)
+    h_ct = np.empty_like(pt)
+    ctx.encrypt_host(pt.ctypes.data, h_ct.ctypes.data, n, pb, chunk_bytes=4 << 20)
+    assert np.array_equal(h_ct, want)
+    h_rt = np.empty_like(pt)
+    ctx.decrypt_host(h_ct.ctypes.data, h_rt.ctypes.data, n, pb, chunk_bytes=4 << 20)
+    assert np.array_equal(h_rt, pt)
+
+
 def test_key_index_array_divergent_waves(torch):
     """Arbitrary per-payload key indices: several keys inside one wave (waterfall)."""
     rng = np.random.default_rng(9)
