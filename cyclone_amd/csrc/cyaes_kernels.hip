@@ -38,7 +38,6 @@ namespace {
 
 // v_perm_b32 selectors: result = (byte k of u) << 8 | lo.byte0 [| lo.byte2 << 16]
 constexpr uint32_t kSel0 = 0x0C0C0400u;
-constexpr uint32_t kSel1 = 0x0C0C0500u;
 constexpr uint32_t kSel2 = 0x0C0C0600u;
 constexpr uint32_t kSel3 = 0x0C0C0700u;
 // Region-1 selectors: byte2 = 0x02 picks lo.byte2 (= 1), i.e. + 64 KiB.
@@ -52,12 +51,23 @@ __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_rotatel
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
-// (a & m) | (b & ~m): v_bfi_b32
-__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+// Per bit m ? a : b.  Always v_bitop3_b32 (truth table over S0 = 0xF0,
+// S1 = 0xCC, S2 = 0xAA): on gfx950 it issues at the full VALU rate, while
+// v_bfi_b32, v_perm_b32, v_and_or_b32 and SDWA forms issue at half of it
+// (tools/valurate.hip, profiles/r01/valurate.jsonl).
+__device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_bitop3_b32(a, m, b, 0xE2);
+}
 
+// Row address of byte k of u: (byte k) << 8 | lane bits (one half-rate v_perm_b32).
 __device__ __forceinline__ uint32_t addr(uint32_t u, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(u, lo, sel);
 }
+// Byte 1 already sits on the row bits: (u & 0xFF00) | lo's other bits, one
+// full-rate op.  lo's byte 2 (= 1) makes it a region-1 address, so the tables
+// indexed by byte 1 live in region 1.
+constexpr uint32_t kRowMask = 0x0000FF00u;
+__device__ __forceinline__ uint32_t addr1(uint32_t u, uint32_t lo) { return sel(kRowMask, u, lo); }
 
 __device__ __forceinline__ uint32_t ld(const char* lds, uint32_t a) {
     return *reinterpret_cast<const uint32_t*>(lds + a);
@@ -83,32 +93,35 @@ __device__ __forceinline__ uint32_t fastdiv(uint32_t n, const Fastdiv& f) {
     return (uint32_t)((hi + (lo >> 32)) >> 32);
 }
 
-// Encrypt middle-round column: all four T-tables resident, no rotation.
-__device__ __forceinline__ uint32_t ecol(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
+// Middle-round column (encrypt TL1..TL4, decrypt TL5..TL8; all four tables
+// resident, no rotation).  Image: region 0 = T1 | T3, region 1 = T2 | T4.
+__device__ __forceinline__ uint32_t tcol(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
                                          uint32_t x3, uint32_t k) {
-    const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));                   // TL1[b0]
-    const uint32_t l1 = ld(lds + kHalfB, addr(x1, lo, kSel1));          // TL2[b1]
-    const uint32_t l2 = ld(lds, addr(x2, lo, region1(kSel2)));          // TL3[b2]
-    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, region1(kSel3))); // TL4[b3]
+    const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));                   // T1[b0]
+    const uint32_t l1 = ld(lds, addr1(x1, lo));                         // T2[b1]
+    const uint32_t l2 = ld(lds + kHalfB, addr(x2, lo, kSel2));          // T3[b2]
+    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, region1(kSel3))); // T4[b3]
     return xor3(l0, l1, xor3(l2, l3, k));
 }
+#define ecol tcol
+#define dcol tcol
 
 // Merge the four last-round bytes (byte j of word j-th lookup).
 __device__ __forceinline__ uint32_t merge4(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3) {
-    return bfi(0x0000FFFFu, bfi(0x000000FFu, l0, l1), bfi(0x00FF0000u, l2, l3));
+    return sel(0x0000FFFFu, sel(0x000000FFu, l0, l1), sel(0x00FF0000u, l2, l3));
 }
 
 // ---- encryption (_encryptBlock, cyr_rijndael.cpp:638-705) -----------------
-// Region 0 rows: A = TL1 (LE bytes 2s,s,s,3s), B = TL2; region 1: A = TL3,
-// B = TL4 (rotl8/16/24 of TL1).  Column j takes b0(u_j), b1(u_j+1),
-// b2(u_j+2), b3(u_j+3) (ShiftRows).  Last round: S[x] is byte0/byte3 of TL3
-// and byte1/byte2 of TL1.
+// Region 0 rows: A = TL1 (LE bytes 2s,s,s,3s), B = TL3; region 1: A = TL2,
+// B = TL4 (TL2/TL3/TL4 = rotl8/16/24 of TL1).  Column j takes b0(u_j),
+// b1(u_j+1), b2(u_j+2), b3(u_j+3) (ShiftRows).  Last round: S[x] is byte 0 of
+// TL3, byte 1 of TL4, byte 2 of TL1 and byte 3 of TL2.
 __device__ __forceinline__ uint32_t enc_last(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
                                              uint32_t x3) {
-    const uint32_t l0 = ld(lds, addr(x0, lo, region1(kSel0)));
-    const uint32_t l1 = ld(lds, addr(x1, lo, kSel1));
-    const uint32_t l2 = ld(lds, addr(x2, lo, kSel2));
-    const uint32_t l3 = ld(lds, addr(x3, lo, region1(kSel3)));
+    const uint32_t l0 = ld(lds + kHalfB, addr(x0, lo, kSel0));   // TL3
+    const uint32_t l1 = ld(lds + kHalfB, addr1(x1, lo));         // TL4
+    const uint32_t l2 = ld(lds, addr(x2, lo, kSel2));            // TL1
+    const uint32_t l3 = ld(lds, addr(x3, lo, region1(kSel3)));   // TL2
     return merge4(l0, l1, l2, l3);
 }
 
@@ -142,17 +155,43 @@ __device__ __forceinline__ void enc_blocks(const char* lds, uint32_t lo, const u
     }
 }
 
+#if CYAES_VALU_FILLER
+// Experiment only (make variant DEFS=-DCYAES_VALU_FILLER=N): N extra full-rate
+// VALU ops per round in 4 independent chains, to measure how much idle VALU
+// issue the LDS-bound rounds leave (and what it costs in clock).
+struct Filler {
+    uint32_t a[4] = {1, 2, 3, 4};
+    __device__ __forceinline__ void run(uint32_t x, uint32_t y) {
+#pragma unroll
+        for (int i = 0; i < CYAES_VALU_FILLER; i++)
+            asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[i & 3]) : "v"(x), "v"(y));
+    }
+    __device__ __forceinline__ uint32_t sum() const { return a[0] ^ a[1] ^ a[2] ^ a[3]; }
+};
+__device__ Filler* g_filler_sink;
+#define FILLER_RUN(x, y) filler.run(x, y)
+#else
+#define FILLER_RUN(x, y)
+#endif
+
 // s = plaintext ^ chain ^ ek[0..3] on entry, ciphertext on exit.
 __device__ __forceinline__ void enc_block(const char* lds, uint32_t lo, const uint32_t* __restrict__ ek,
                                           uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
+#if CYAES_VALU_FILLER
+    Filler filler;
+#endif
 #pragma unroll
     for (int r = 1; r < 10; r++) {
         const uint32_t a0 = ecol(lds, lo, s0, s1, s2, s3, ek[4 * r + 0]);
         const uint32_t a1 = ecol(lds, lo, s1, s2, s3, s0, ek[4 * r + 1]);
         const uint32_t a2 = ecol(lds, lo, s2, s3, s0, s1, ek[4 * r + 2]);
         const uint32_t a3 = ecol(lds, lo, s3, s0, s1, s2, ek[4 * r + 3]);
+        FILLER_RUN(s0, s2);
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     }
+#if CYAES_VALU_FILLER
+    if (filler.sum() == 0x9E3779B9u && lo == 0xFFFFFFFFu) g_filler_sink->a[0] = 1;  // never true: keeps the work
+#endif
     const uint32_t o0 = enc_last(lds, lo, s0, s1, s2, s3) ^ ek[40];
     const uint32_t o1 = enc_last(lds, lo, s1, s2, s3, s0) ^ ek[41];
     const uint32_t o2 = enc_last(lds, lo, s2, s3, s0, s1) ^ ek[42];
@@ -164,37 +203,33 @@ __device__ __forceinline__ void enc_block(const char* lds, uint32_t lo, const ui
 // TL5 has LE bytes (14s, 9s, 13s, 11s); TL6/TL7/TL8 = rotl8/16/24 of it.
 // Column j takes b0(u_j), b1(u_j-1), b2(u_j-2), b3(u_j-3) (inverse
 // ShiftRows, cyr_rijndael.cpp:731-746).
-// 160 KiB decrypt image: region 0 = TL5 | TL6, region 1 = TL7 | TL8 (TL6/TL8
-// = rotl8 of TL5/TL7, made during the fill), so a middle-round column needs
-// no rotation (as ecol; A/B vs the 128 KiB TL5|TL7 image with one rotation
+// 160 KiB decrypt image: region 0 = TL5 | TL7, region 1 = TL6 | TL8 (TL6/TL8
+// = rotl8 of TL5/TL7, made during the fill), so a middle-round column is
+// tcol, as encrypt's (A/B vs the 128 KiB TL5|TL7 image with one rotation
 // per column: same LDS cycles, -1.2 % time from the higher clock), and Si at
-// 128 KiB in 128-B rows (32 slots), addressed as (perm(u, lo, sel) >> 1):
-// lo = [lane*4, lane*8, 1, 4] gives x << 8 | lane*8 | 4 << 16 before the shift.
-__device__ __forceinline__ uint32_t dec_lo(uint32_t tid) {
-    return ((tid & 31u) << 2) | ((tid & 31u) << 11) | 0x10000u | 0x04000000u;
+// 128 KiB in 128-B rows (32 slots): x << 7 | lane*4 | 128 KiB, built with one
+// full-rate shift and one sel (addr_si).
+__device__ __forceinline__ uint32_t dec_lo(uint32_t tid) { return ((tid & 31u) << 2) | 0x10000u; }
+constexpr uint32_t kSiRowMask = 0x00007F80u;
+template <int K>  // byte K of u
+__device__ __forceinline__ uint32_t addr_si(uint32_t u, uint32_t lsi) {
+    const uint32_t r = K == 0 ? u << 7 : u >> (8 * K - 7);
+    return sel(kSiRowMask, r, lsi);
 }
-__device__ __forceinline__ uint32_t dcol(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
-                                         uint32_t x3, uint32_t k) {
-    const uint32_t l0 = ld(lds, addr(x0, lo, kSel0));                   // TL5[b0]
-    const uint32_t l1 = ld(lds + kHalfB, addr(x1, lo, kSel1));          // TL6[b1]
-    const uint32_t l2 = ld(lds, addr(x2, lo, region1(kSel2)));          // TL7[b2]
-    const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, region1(kSel3))); // TL8[b3]
-    return xor3(l0, l1, xor3(l2, l3, k));
-}
-__device__ __forceinline__ uint32_t dec_last(const char* lds, uint32_t lo, uint32_t x0, uint32_t x1, uint32_t x2,
+__device__ __forceinline__ uint32_t dec_last(const char* lds, uint32_t lsi, uint32_t x0, uint32_t x1, uint32_t x2,
                                              uint32_t x3) {
-    const uint32_t l0 = ld(lds, addr(x0, lo, 0x0C030401u) >> 1);
-    const uint32_t l1 = ld(lds, addr(x1, lo, 0x0C030501u) >> 1);
-    const uint32_t l2 = ld(lds, addr(x2, lo, 0x0C030601u) >> 1);
-    const uint32_t l3 = ld(lds, addr(x3, lo, 0x0C030701u) >> 1);
+    const uint32_t l0 = ld(lds, addr_si<0>(x0, lsi));
+    const uint32_t l1 = ld(lds, addr_si<1>(x1, lsi));
+    const uint32_t l2 = ld(lds, addr_si<2>(x2, lsi));
+    const uint32_t l3 = ld(lds, addr_si<3>(x3, lsi));
     return merge4(l0, l1, l2, l3);
 }
 __device__ __forceinline__ void fill_dec_image(uint32_t* lds, const uint32_t* __restrict__ t) {
     uint4* l4 = reinterpret_cast<uint4*>(lds);
     for (int q = threadIdx.x; q < 8192; q += blockDim.x) {  // two 64 KiB T regions
         const int region = q >> 12, half = (q >> 3) & 1, row = (q >> 4) & 255;
-        uint32_t v = t[256 * region + row];
-        if (half) v = rotl8(v);
+        uint32_t v = t[256 * half + row];
+        if (region) v = rotl8(v);
         l4[q] = make_uint4(v, v, v, v);
     }
     for (int q = threadIdx.x; q < 2048; q += blockDim.x) {  // Si: 256 rows x 128 B
@@ -236,10 +271,11 @@ __device__ __forceinline__ void dec_cbc(const char* lds, uint32_t lo, const uint
     }
 #pragma unroll
     for (int n = 0; n < N; n++) {
-        prev[n] = make_uint4(xor3(dec_last(lds, lo, s[n][0], s[n][3], s[n][2], s[n][1]), dk[40], prev[n].x),
-                             xor3(dec_last(lds, lo, s[n][1], s[n][0], s[n][3], s[n][2]), dk[41], prev[n].y),
-                             xor3(dec_last(lds, lo, s[n][2], s[n][1], s[n][0], s[n][3]), dk[42], prev[n].z),
-                             xor3(dec_last(lds, lo, s[n][3], s[n][2], s[n][1], s[n][0]), dk[43], prev[n].w));
+        const uint32_t lsi = (lo & 0xFFu) | 0x20000u;  // lane bits | 128 KiB (Si image)
+        prev[n] = make_uint4(xor3(dec_last(lds, lsi, s[n][0], s[n][3], s[n][2], s[n][1]), dk[40], prev[n].x),
+                             xor3(dec_last(lds, lsi, s[n][1], s[n][0], s[n][3], s[n][2]), dk[41], prev[n].y),
+                             xor3(dec_last(lds, lsi, s[n][2], s[n][1], s[n][0], s[n][3]), dk[42], prev[n].z),
+                             xor3(dec_last(lds, lsi, s[n][3], s[n][2], s[n][1], s[n][0]), dk[43], prev[n].w));
     }
 }
 
@@ -361,8 +397,8 @@ __device__ __forceinline__ void drain_loads() { asm volatile("s_waitcnt vmcnt(0)
 template <bool RAGGED, bool KEYED>
 __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
-    fill_region(lds_words, a.tables, a.tables + 256, blockDim.x);
-    fill_region(lds_words + 16384, a.tables + 512, a.tables + 768, blockDim.x);
+    fill_region(lds_words, a.tables, a.tables + 512, blockDim.x);              // TL1 | TL3
+    fill_region(lds_words + 16384, a.tables + 256, a.tables + 768, blockDim.x);  // TL2 | TL4
     __shared__ uint32_t lead;  // prio_feedback
     if (threadIdx.x == 0) lead = 0;
     uint32_t prog = 0;
