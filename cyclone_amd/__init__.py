@@ -107,6 +107,7 @@ _SIGS = {
     "cyaes_batcher_submit_seal": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_int32, _vp, ctypes.c_uint32, _vp,
                                                  _vp, _vp]),
     "cyaes_batcher_submit_open": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp]),
+    "cyaes_batcher_submit_many": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
     "cyaes_batcher_flush": (ctypes.c_int, [_vp]),
     "cyaes_batcher_stats": (ctypes.c_int, [_vp, _u64p]),
 }
@@ -409,9 +410,16 @@ OP_ENCRYPT, OP_DECRYPT, OP_RELAY_SEAL, OP_RELAY_OPEN = 0, 1, 2, 3
 _DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)
 
 
+class BatchReq(ctypes.Structure):
+    """struct cyaes_batch_req (cyaes_batcher_submit_many)."""
+
+    _fields_ = [("op", ctypes.c_int), ("slot", ctypes.c_uint32), ("conn_id", ctypes.c_int32), ("inp", _vp),
+                ("out", _vp), ("size", ctypes.c_uint32), ("done", _DONE_FN), ("user", _vp)]
+
+
 class BatcherConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("max_batch_bytes", ctypes.c_uint32),
-                ("max_delay_us", ctypes.c_uint32), ("inflight", ctypes.c_uint32)]
+                ("max_delay_us", ctypes.c_uint32), ("inflight", ctypes.c_uint32), ("workers", ctypes.c_uint32)]
 
 
 class Batcher:
@@ -421,9 +429,9 @@ class Batcher:
     alive by the batcher until the request completes.  `done(status)` runs on
     the batcher's completion thread."""
 
-    def __init__(self, device=0, max_batch_bytes=0, max_delay_us=0, inflight=0, lib=None):
+    def __init__(self, device=0, max_batch_bytes=0, max_delay_us=0, inflight=0, workers=0, lib=None):
         self._lib = lib if lib is not None else load_library()
-        cfg = BatcherConfig(device, max_batch_bytes, max_delay_us, inflight)
+        cfg = BatcherConfig(device, max_batch_bytes, max_delay_us, inflight, workers)
         h = _vp()
         _check(self._lib.cyaes_batcher_create(ctypes.byref(cfg), ctypes.byref(h)), "cyaes_batcher_create")
         self._h = h
@@ -502,6 +510,31 @@ class Batcher:
         if st:
             self._untrack(token)
             raise CyaesError(st, "submit_open")
+
+    def submit_many(self, reqs):
+        """reqs: [(op, slot, inp, out, size_or_None, done, conn_id)] in one call
+        (cyaes_batcher_submit_many).  Returns the per-request status list; a
+        request with a non-zero status was not accepted (its done never runs)."""
+        n = len(reqs)
+        arr = (BatchReq * max(1, n))()
+        tokens = []
+        for i, (op, slot, inp, out, size, done, conn) in enumerate(reqs):
+            if op == OP_RELAY_OPEN:
+                src = dst = _Buf(out if out is not None else inp, True)
+            else:
+                src = _Buf(inp, False)
+                dst = src if out is inp else _Buf(out, True)
+            if size is None:
+                size = src.n
+            token = self._track((src, dst), done)
+            tokens.append(token)
+            arr[i] = BatchReq(op, slot, conn or 0, src.ptr, dst.ptr, size, self._cb, token)
+        st = (ctypes.c_int * max(1, n))()
+        self._lib.cyaes_batcher_submit_many(self._h, arr, n, st)
+        for i, token in enumerate(tokens):
+            if st[i]:
+                self._untrack(token)
+        return [int(st[i]) for i in range(n)]
 
     def flush(self):
         """Waits for every request submitted so far; returns the first error status (0 = none)."""

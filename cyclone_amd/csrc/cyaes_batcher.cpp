@@ -6,12 +6,17 @@
 // Rijndael pair per pipe created after the DH handshake
 // (relay_server.cpp:218-240) and deleted on close (:370-375).
 //
-// Threads: callers submit into a queue; the builder thread closes a batch
-// when it is full, when its oldest request has waited max_delay_us, or when
-// someone flushes, gathers it into a pinned staging buffer and launches
-// H2D -> ragged encrypt -> ragged decrypt -> D2H on that stage's stream; the
-// completion thread waits for the stage, scatters outputs, runs callbacks and
-// recycles the stage.  Staging layout of one batch (one H2D, one D2H):
+// Threads: callers submit into one of kShards queues (the shard of the
+// calling thread, so a thread's requests stay in order; one short shard lock
+// per submit call, never the batcher's lock, and submit_many takes it once
+// for many requests); the builder thread closes a batch when it is full, when
+// its oldest request has waited max_delay_us, or when someone flushes -- it
+// swaps the shard queues out and forms the batch outside every lock -- gathers it into a
+// pinned staging buffer and launches H2D -> ragged encrypt -> ragged decrypt
+// -> D2H on that stage's stream; the completion thread waits for the stage,
+// scatters outputs, runs callbacks and recycles the stage.  Gather and
+// scatter of large batches are split over `workers` threads (Pool).
+// Staging layout of one batch (one H2D, one D2H):
 //   [data: each request 16-B aligned][enc meta][dec meta][key schedules]
 // A SEAL/OPEN request keeps its packet at data offset o + 4 so the payload
 // (packet offset 12) sits at o + 16.
@@ -20,6 +25,8 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <functional>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -73,6 +80,98 @@ int map_err(hipError_t e) {
     return (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? CYAES_ENOMEM : CYAES_EDEVICE;
 }
 
+// Fixed worker threads for the gather / scatter copies of one stage: run(n, fn)
+// calls fn(begin, end) over [0, n) in chunks, on the workers and the caller,
+// and returns when all chunks are done.  One job at a time per pool.
+class Pool {
+  public:
+    explicit Pool(int workers) {
+        for (int i = 0; i < workers; i++) th_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    template <typename F>
+    void run(size_t n, size_t chunk, F&& f) {
+        if (th_.empty() || n <= chunk) {
+            f(0, n);
+            return;
+        }
+        std::function<void(size_t, size_t)> fn(std::forward<F>(f));
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &fn;
+            n_ = n;
+            chunk_ = chunk;
+            next_.store(0);
+            active_ = (int)th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        work(fn, n, chunk);
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_done_.wait(lk, [&] { return active_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void work(const std::function<void(size_t, size_t)>& fn, size_t n, size_t chunk) {
+        for (;;) {
+            const size_t b = next_.fetch_add(chunk);
+            if (b >= n) return;
+            fn(b, std::min(n, b + chunk));
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            const auto* fn = fn_;
+            const size_t n = n_, chunk = chunk_;
+            lk.unlock();
+            work(*fn, n, chunk);
+            lk.lock();
+            if (--active_ == 0) cv_done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, cv_done_;
+    const std::function<void(size_t, size_t)>* fn_ = nullptr;
+    size_t n_ = 0, chunk_ = 0;
+    std::atomic<size_t> next_{0};
+    int active_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// Requests per gather/scatter chunk: splitting pays only for large batches.
+constexpr size_t kCopyChunk = 64;
+
+// Submission shards: with one queue and one lock, 8 relay-style threads
+// resubmitting ~1 M requests/s convoyed on the lock (tools/bench_batcher.cpp).
+constexpr int kShards = 16;
+struct alignas(64) Shard {
+    std::mutex mu;
+    std::vector<Req> q;
+};
+int my_shard() {
+    static std::atomic<int> next{0};
+    thread_local int s = next.fetch_add(1) % kShards;
+    return s;
+}
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
+
 }  // namespace
 
 struct cyaes_batcher {
@@ -81,20 +180,28 @@ struct cyaes_batcher {
     uint64_t stage_cap = 0;
     std::vector<Stage> stages;
 
+    // Submission: shard queues + counters (lock-free for submitters except their shard).
+    std::array<Shard, kShards> shards;
+    std::atomic<int64_t> queued_reqs{0}, queued_bytes{0};  // transiently negative while a drain races an enqueue
+    std::atomic<int64_t> oldest_ns{0};  // submit time of the oldest queued request (0: none recorded)
+    std::atomic<uint64_t> submitted{0};
+    std::atomic<int> flushers{0};
+    std::atomic<bool> stop{false};
+
+    // Builder / completion hand-off, stats, flush (guarded by mu).
     std::mutex mu;
     std::condition_variable cv_submit, cv_free, cv_inflight, cv_flush;
-    std::deque<Req> queue;
-    uint64_t queued_bytes = 0;
     std::vector<Stage*> free_stages;
     std::deque<Stage*> inflight;
-    bool stop = false, builder_done = false;
-    int flushers = 0;
-    uint64_t submitted = 0, completed = 0;
+    bool builder_done = false;
+    uint64_t completed = 0;
     uint64_t batches = 0, bytes = 0, max_batch = 0, errors = 0;
     int first_error = CYAES_OK;
 
+    std::mutex smu;  // session table
     std::vector<std::shared_ptr<const Sched>> sessions;  // nullptr = free slot
 
+    std::unique_ptr<Pool> gather_pool, scatter_pool;
     std::thread builder, completer;
 
     // Cost of a request in a stage: data + meta (16 B) + a schedule if its key is new to the batch.
@@ -103,25 +210,56 @@ struct cyaes_batcher {
     void build_loop();
     void complete_loop();
     int launch(Stage* st);
-    int submit(Req&& r);
+    int make(const cyaes_batch_req& q, Req* r);
+    void enqueue(Req* rs, size_t n, uint64_t nbytes);
 };
 
 void cyaes_batcher::build_loop() {
-    std::unique_lock<std::mutex> lk(mu);
+    std::vector<Req> carry;  // builder-private: taken from the shards, not yet batched (older than the shards)
+    size_t cpos = 0;
+    std::unordered_map<const Sched*, int> seen;
     for (;;) {
-        cv_submit.wait(lk, [&] { return stop || !queue.empty(); });
-        if (queue.empty()) break;  // stop requested and drained
-        // Let the batch fill: until it is full, the oldest request is due, or a flush/stop.
-        const auto due = queue.front().t + std::chrono::microseconds(cfg.max_delay_us);
-        cv_submit.wait_until(lk, due, [&] { return stop || flushers > 0 || queued_bytes >= cfg.max_batch_bytes; });
-        cv_free.wait(lk, [&] { return !free_stages.empty(); });
-        Stage* st = free_stages.back();
-        free_stages.pop_back();
+        Stage* st = nullptr;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            if (cpos == carry.size()) {
+                carry.clear();
+                cpos = 0;
+                cv_submit.wait(lk, [&] { return stop || queued_reqs.load() > 0; });
+                if (queued_reqs.load() <= 0) break;  // stop requested and drained
+                // Let the batch fill: until it is full, the oldest request is due, or a flush/stop.
+                const int64_t t = oldest_ns.load();
+                const auto due = Clock::time_point(std::chrono::nanoseconds(t ? t : now_ns())) +
+                                 std::chrono::microseconds(cfg.max_delay_us);
+                cv_submit.wait_until(lk, due, [&] {
+                    return stop || flushers.load() > 0 || queued_bytes.load() >= (int64_t)cfg.max_batch_bytes;
+                });
+            }
+            cv_free.wait(lk, [&] { return !free_stages.empty(); });
+            st = free_stages.back();
+            free_stages.pop_back();
+        }
+        // Take every shard's queue (a swap under each shard lock).
+        oldest_ns.store(0);
+        int64_t took = 0, took_bytes = 0;
+        for (Shard& sh : shards) {
+            std::vector<Req> q;
+            {
+                std::lock_guard<std::mutex> lk(sh.mu);
+                q.swap(sh.q);
+            }
+            for (const Req& r : q) took_bytes += r.data_bytes();
+            took += (int64_t)q.size();
+            if (carry.empty()) carry.swap(q);
+            else carry.insert(carry.end(), std::make_move_iterator(q.begin()), std::make_move_iterator(q.end()));
+        }
+        queued_reqs.fetch_sub(took);
+        queued_bytes.fetch_sub(took_bytes);
         st->reqs.clear();
         uint64_t used = 0, data = 0;
-        std::unordered_map<const Sched*, int> seen;
-        while (!queue.empty()) {
-            const Req& r = queue.front();
+        seen.clear();
+        for (; cpos < carry.size(); cpos++) {
+            Req& r = carry[cpos];
             const bool new_key = !seen.count(r.key.get());
             const uint64_t c = cost(r) + (new_key ? sizeof(Sched) : 0);
             if (!st->reqs.empty() && (data + r.data_bytes() > cfg.max_batch_bytes || used + c + 64 > stage_cap))
@@ -129,16 +267,19 @@ void cyaes_batcher::build_loop() {
             if (new_key) seen.emplace(r.key.get(), 0);
             used += c;
             data += r.data_bytes();
-            queued_bytes -= r.data_bytes();
-            st->reqs.push_back(std::move(queue.front()));
-            queue.pop_front();
+            st->reqs.push_back(std::move(r));
         }
-        lk.unlock();
+        if (st->reqs.empty()) {  // raced: nothing taken (cannot happen with took > 0 or carry)
+            std::lock_guard<std::mutex> lk(mu);
+            free_stages.push_back(st);
+            continue;
+        }
         st->status = launch(st);
-        lk.lock();
+        std::lock_guard<std::mutex> lk(mu);
         inflight.push_back(st);
         cv_inflight.notify_one();
     }
+    std::lock_guard<std::mutex> lk(mu);
     builder_done = true;
     cv_inflight.notify_all();
 }
@@ -153,25 +294,10 @@ int cyaes_batcher::launch(Stage* st) {
     std::unordered_map<const Sched*, uint32_t> kidx;
     std::vector<const Sched*> klist;
     uint64_t pos = 0;
-    for (size_t i = 0; i < n; i++) {
+    for (size_t i = 0; i < n; i++) {  // layout pass (the copies run below, in parallel)
         const Req& r = st->reqs[i];
         st->off[i] = pos;
-        uint8_t* dst = st->h + pos;
-        uint64_t coff = pos;  // where the kernel works
-        switch (r.op) {
-            case CYAES_OP_ENCRYPT:
-            case CYAES_OP_DECRYPT:
-                memcpy(dst, r.in, r.size);
-                break;
-            case CYAES_OP_RELAY_SEAL:  // relay_local.cpp:189-201: packet build + 0xCE padding
-                cyaes_relay_build_forward(dst + 4, r.conn, r.in, r.size);
-                coff = pos + 16;
-                break;
-            case CYAES_OP_RELAY_OPEN:
-                memcpy(dst + 4, r.in, r.size);
-                coff = pos + 16;
-                break;
-        }
+        const uint64_t coff = r.op >= CYAES_OP_RELAY_SEAL ? pos + 16 : pos;  // where the kernel works
         pos += r.data_bytes();
         if (r.crypt == 0) continue;  // size 0: a no-op (cyr_rijndael.cpp:600 loop never runs)
         auto it = kidx.find(r.key.get());
@@ -189,6 +315,24 @@ int cyaes_batcher::launch(Stage* st) {
         (dec ? dk : ek).push_back(k);
     }
     st->data_end = pos;
+    gather_pool->run(n, kCopyChunk, [st](size_t b, size_t e) {
+        for (size_t i = b; i < e; i++) {
+            const Req& r = st->reqs[i];
+            uint8_t* dst = st->h + st->off[i];
+            switch (r.op) {
+                case CYAES_OP_ENCRYPT:
+                case CYAES_OP_DECRYPT:
+                    memcpy(dst, r.in, r.size);
+                    break;
+                case CYAES_OP_RELAY_SEAL:  // relay_local.cpp:189-201: packet build + 0xCE padding
+                    cyaes_relay_build_forward(dst + 4, r.conn, r.in, r.size);
+                    break;
+                case CYAES_OP_RELAY_OPEN:
+                    memcpy(dst + 4, r.in, r.size);
+                    break;
+            }
+        }
+    });
     // Encrypt runs one chain per lane and waterfalls over the distinct keys of
     // a wave (cyaes_kernels.hip, k_encrypt), so order its list by key: a wave
     // then sees one key, two at a boundary, instead of one per looper thread.
@@ -267,24 +411,28 @@ void cyaes_batcher::complete_loop() {
         lk.unlock();
         int status = st->status;
         if (status == CYAES_OK) status = map_err(hipEventSynchronize(st->done));
-        uint64_t nbytes = 0;
-        for (size_t i = 0; i < st->reqs.size(); i++) {
-            const Req& r = st->reqs[i];
-            const uint8_t* src = st->h + st->off[i];
-            if (status == CYAES_OK) {
-                switch (r.op) {
-                    case CYAES_OP_ENCRYPT:
-                    case CYAES_OP_DECRYPT:
-                        memcpy(r.out, src, r.size);
-                        break;
-                    case CYAES_OP_RELAY_SEAL:
-                        memcpy(r.out, src + 4, CYAES_RELAY_PAYLOAD_OFFSET + r.crypt);
-                        break;
-                    case CYAES_OP_RELAY_OPEN:  // header untouched, payload decrypted in place
-                        memcpy(r.out + CYAES_RELAY_PAYLOAD_OFFSET, src + 16, r.crypt);
-                        break;
+        if (status == CYAES_OK) {
+            scatter_pool->run(st->reqs.size(), kCopyChunk, [st](size_t b, size_t e) {
+                for (size_t i = b; i < e; i++) {
+                    const Req& r = st->reqs[i];
+                    const uint8_t* src = st->h + st->off[i];
+                    switch (r.op) {
+                        case CYAES_OP_ENCRYPT:
+                        case CYAES_OP_DECRYPT:
+                            memcpy(r.out, src, r.size);
+                            break;
+                        case CYAES_OP_RELAY_SEAL:
+                            memcpy(r.out, src + 4, CYAES_RELAY_PAYLOAD_OFFSET + r.crypt);
+                            break;
+                        case CYAES_OP_RELAY_OPEN:  // header untouched, payload decrypted in place
+                            memcpy(r.out + CYAES_RELAY_PAYLOAD_OFFSET, src + 16, r.crypt);
+                            break;
+                    }
                 }
-            }
+            });
+        }
+        uint64_t nbytes = 0;
+        for (const Req& r : st->reqs) {  // callbacks in batch order, on this thread
             nbytes += r.crypt;
             if (r.done) r.done(r.user, status);
         }
@@ -305,15 +453,71 @@ void cyaes_batcher::complete_loop() {
     }
 }
 
-int cyaes_batcher::submit(Req&& r) {
-    r.t = Clock::now();
-    std::lock_guard<std::mutex> lk(mu);
-    if (stop) return CYAES_EINVAL;
-    queued_bytes += r.data_bytes();
-    submitted++;
-    queue.push_back(std::move(r));
-    if (queue.size() == 1 || queued_bytes >= cfg.max_batch_bytes) cv_submit.notify_one();
+// Validates one request and pins its session's schedule (caller holds smu).
+int cyaes_batcher::make(const cyaes_batch_req& q, Req* r) {
+    *r = Req{};
+    switch (q.op) {
+        case CYAES_OP_ENCRYPT:
+        case CYAES_OP_DECRYPT:
+            if (q.size % 16 || q.size > cfg.max_batch_bytes || (q.size && (!q.in || !q.out))) return CYAES_EINVAL;
+            r->size = r->crypt = q.size;
+            r->in = q.in;
+            r->out = q.out;
+            break;
+        case CYAES_OP_RELAY_SEAL:
+            if (!q.out || q.size > CYAES_RELAY_MAX_CHUNK || (q.size && !q.in)) return CYAES_EINVAL;
+            r->in = q.in;
+            r->out = q.out;
+            r->size = q.size;
+            r->crypt = cyaes_relay_round16(q.size);
+            r->conn = q.conn_id;
+            break;
+        case CYAES_OP_RELAY_OPEN: {
+            uint8_t* packet = q.out ? q.out : const_cast<uint8_t*>(q.in);
+            if (!packet || q.size < CYAES_RELAY_PAYLOAD_OFFSET) return CYAES_EINVAL;
+            const uint32_t psize = (uint32_t)((packet[0] << 8) | packet[1]);  // BE u16 (cye_packet.cpp:82-86)
+            const uint32_t pid = (uint32_t)((packet[2] << 8) | packet[3]);
+            if (pid != CYAES_RELAY_FORWARD || psize + CYAES_RELAY_HEADSIZE != q.size || psize < 8 || (psize - 8) % 16)
+                return CYAES_EINVAL;
+            r->in = packet;
+            r->out = packet;
+            r->size = q.size;
+            r->crypt = psize - 8u;  // relay_server.cpp:329: packet_size - sizeof(RelayForwardMsg)
+            break;
+        }
+        default:
+            return CYAES_EINVAL;
+    }
+    if (q.slot >= sessions.size() || !sessions[q.slot]) return CYAES_ERANGE;
+    r->op = (uint8_t)q.op;
+    r->key = sessions[q.slot];
+    r->done = q.done;
+    r->user = q.user;
     return CYAES_OK;
+}
+
+// Appends n requests to the calling thread's shard (one lock) and wakes the
+// builder when the queue was empty or the batch is now full.
+void cyaes_batcher::enqueue(Req* rs, size_t n, uint64_t nbytes) {
+    if (n == 0) return;
+    const auto t = Clock::now();
+    Shard& sh = shards[my_shard()];
+    {
+        std::lock_guard<std::mutex> lk(sh.mu);
+        for (size_t i = 0; i < n; i++) {
+            rs[i].t = t;
+            sh.q.push_back(std::move(rs[i]));
+        }
+    }
+    submitted.fetch_add(n);
+    int64_t zero = 0;
+    oldest_ns.compare_exchange_strong(zero, now_ns());
+    const int64_t before = queued_reqs.fetch_add((int64_t)n);
+    const int64_t b0 = queued_bytes.fetch_add((int64_t)nbytes), cap = cfg.max_batch_bytes;
+    if (before <= 0 || (b0 < cap && b0 + (int64_t)nbytes >= cap)) {
+        std::lock_guard<std::mutex> lk(mu);  // orders the wake-up after the builder's predicate check
+        cv_submit.notify_one();
+    }
 }
 
 extern "C" {
@@ -325,7 +529,9 @@ int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out) {
     if (c.max_batch_bytes == 0) c.max_batch_bytes = 32u << 20;
     if (c.max_delay_us == 0) c.max_delay_us = 100;
     if (c.inflight == 0) c.inflight = 3;
-    if (c.max_batch_bytes < 4096 || c.max_batch_bytes > (1u << 30) || c.inflight > 16) return CYAES_EINVAL;
+    if (c.workers == 0) c.workers = 4;
+    if (c.max_batch_bytes < 4096 || c.max_batch_bytes > (1u << 30) || c.inflight > 16 || c.workers > 64)
+        return CYAES_EINVAL;
     cyaes_gpu* ctx = nullptr;
     int st = cyaes_gpu_create(c.device, &ctx);
     if (st) return st;
@@ -353,6 +559,8 @@ int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out) {
         cyaes_batcher_destroy(b);
         return map_err(e);
     }
+    b->gather_pool.reset(new Pool((int)c.workers - 1));  // + the builder thread itself
+    b->scatter_pool.reset(new Pool((int)c.workers - 1)); // + the completion thread itself
     b->builder = std::thread([b] {
         (void)hipSetDevice(b->cfg.device);
         b->build_loop();
@@ -369,7 +577,7 @@ void cyaes_batcher_destroy(cyaes_batcher* b) {
     if (!b) return;
     {
         std::lock_guard<std::mutex> lk(b->mu);
-        b->stop = true;
+        b->stop.store(true);
     }
     b->cv_submit.notify_all();
     if (b->builder.joinable()) b->builder.join();
@@ -391,7 +599,7 @@ int cyaes_batcher_session_open(cyaes_batcher* b, const uint8_t key[16], uint32_t
     cyaes::expand_key(key, &k);
     auto s = std::make_shared<Sched>();
     cyaes::to_device_schedule(k, s->data());
-    std::lock_guard<std::mutex> lk(b->mu);
+    std::lock_guard<std::mutex> lk(b->smu);
     size_t i = 0;
     while (i < b->sessions.size() && b->sessions[i]) i++;
     if (i == b->sessions.size()) b->sessions.emplace_back();
@@ -402,82 +610,75 @@ int cyaes_batcher_session_open(cyaes_batcher* b, const uint8_t key[16], uint32_t
 
 int cyaes_batcher_session_close(cyaes_batcher* b, uint32_t slot) {
     if (!b) return CYAES_EINVAL;
-    std::lock_guard<std::mutex> lk(b->mu);
+    std::lock_guard<std::mutex> lk(b->smu);
     if (slot >= b->sessions.size() || !b->sessions[slot]) return CYAES_ERANGE;
     b->sessions[slot].reset();
     return CYAES_OK;
 }
 
-static int session_key(cyaes_batcher* b, uint32_t slot, std::shared_ptr<const Sched>* key) {
-    std::lock_guard<std::mutex> lk(b->mu);
-    if (slot >= b->sessions.size() || !b->sessions[slot]) return CYAES_ERANGE;
-    *key = b->sessions[slot];
+static int submit_one(cyaes_batcher* b, const cyaes_batch_req& q) {
+    if (b->stop.load()) return CYAES_EINVAL;
+    Req r;
+    int st;
+    {
+        std::lock_guard<std::mutex> lk(b->smu);
+        st = b->make(q, &r);
+    }
+    if (st) return st;
+    b->enqueue(&r, 1, r.data_bytes());
     return CYAES_OK;
 }
 
 int cyaes_batcher_submit(cyaes_batcher* b, int op, uint32_t slot, const uint8_t* in, uint8_t* out, size_t size,
                          cyaes_done_fn done, void* user) {
-    if (!b || (op != CYAES_OP_ENCRYPT && op != CYAES_OP_DECRYPT) || size % 16 || size > b->cfg.max_batch_bytes ||
-        (size && (!in || !out)))
-        return CYAES_EINVAL;
-    Req r{};
-    int st = session_key(b, slot, &r.key);
-    if (st) return st;
-    r.op = (uint8_t)op;
-    r.in = in;
-    r.out = out;
-    r.size = r.crypt = (uint32_t)size;
-    r.done = done;
-    r.user = user;
-    return b->submit(std::move(r));
+    if (!b || (op != CYAES_OP_ENCRYPT && op != CYAES_OP_DECRYPT) || size > 0xFFFFFFFFu) return CYAES_EINVAL;
+    return submit_one(b, cyaes_batch_req{op, slot, 0, in, out, (uint32_t)size, done, user});
 }
 
 int cyaes_batcher_submit_seal(cyaes_batcher* b, uint32_t slot, int32_t conn_id, const uint8_t* payload,
                               uint32_t size, uint8_t* packet_out, cyaes_done_fn done, void* user) {
-    if (!b || !packet_out || size > CYAES_RELAY_MAX_CHUNK || (size && !payload)) return CYAES_EINVAL;
-    Req r{};
-    int st = session_key(b, slot, &r.key);
-    if (st) return st;
-    r.op = CYAES_OP_RELAY_SEAL;
-    r.in = payload;
-    r.out = packet_out;
-    r.size = size;
-    r.crypt = cyaes_relay_round16(size);
-    r.conn = conn_id;
-    r.done = done;
-    r.user = user;
-    return b->submit(std::move(r));
+    if (!b) return CYAES_EINVAL;
+    return submit_one(b, cyaes_batch_req{CYAES_OP_RELAY_SEAL, slot, conn_id, payload, packet_out, size, done, user});
 }
 
 int cyaes_batcher_submit_open(cyaes_batcher* b, uint32_t slot, uint8_t* packet, uint32_t packet_bytes,
                               cyaes_done_fn done, void* user) {
-    if (!b || !packet || packet_bytes < CYAES_RELAY_PAYLOAD_OFFSET) return CYAES_EINVAL;
-    const uint32_t psize = (uint32_t)((packet[0] << 8) | packet[1]);  // BE u16 (cye_packet.cpp:82-86)
-    const uint32_t pid = (uint32_t)((packet[2] << 8) | packet[3]);
-    if (pid != CYAES_RELAY_FORWARD || psize + CYAES_RELAY_HEADSIZE != packet_bytes || psize < 8 ||
-        (psize - 8) % 16)
-        return CYAES_EINVAL;
-    Req r{};
-    int st = session_key(b, slot, &r.key);
-    if (st) return st;
-    r.op = CYAES_OP_RELAY_OPEN;
-    r.in = packet;
-    r.out = packet;
-    r.size = packet_bytes;
-    r.crypt = psize - 8u;  // relay_server.cpp:329: packet_size - sizeof(RelayForwardMsg)
-    r.done = done;
-    r.user = user;
-    return b->submit(std::move(r));
+    if (!b) return CYAES_EINVAL;
+    return submit_one(b, cyaes_batch_req{CYAES_OP_RELAY_OPEN, slot, 0, packet, packet, packet_bytes, done, user});
+}
+
+int cyaes_batcher_submit_many(cyaes_batcher* b, const cyaes_batch_req* reqs, uint32_t n, int* status) {
+    if (!b || (n && !reqs)) return CYAES_EINVAL;
+    if (b->stop.load()) return CYAES_EINVAL;
+    std::vector<Req> rs(n);
+    size_t k = 0;
+    uint64_t nbytes = 0;
+    int first = CYAES_OK;
+    {
+        std::lock_guard<std::mutex> lk(b->smu);
+        for (uint32_t i = 0; i < n; i++) {
+            const int st = b->make(reqs[i], &rs[k]);
+            if (status) status[i] = st;
+            if (st) {
+                if (first == CYAES_OK) first = st;
+                continue;
+            }
+            nbytes += rs[k].data_bytes();
+            k++;
+        }
+    }
+    b->enqueue(rs.data(), k, nbytes);
+    return first;
 }
 
 int cyaes_batcher_flush(cyaes_batcher* b) {
     if (!b) return CYAES_EINVAL;
     std::unique_lock<std::mutex> lk(b->mu);
-    const uint64_t target = b->submitted;
-    b->flushers++;
+    const uint64_t target = b->submitted.load();
+    b->flushers.fetch_add(1);
     b->cv_submit.notify_all();
     b->cv_flush.wait(lk, [&] { return b->completed >= target; });
-    b->flushers--;
+    b->flushers.fetch_sub(1);
     const int err = b->first_error;
     b->first_error = CYAES_OK;
     return err;
@@ -491,7 +692,7 @@ int cyaes_batcher_stats(cyaes_batcher* b, uint64_t out[6]) {
     out[2] = b->bytes;
     out[3] = b->max_batch;
     out[4] = b->errors;
-    out[5] = b->submitted - b->completed;
+    out[5] = b->submitted.load() - b->completed;
     return CYAES_OK;
 }
 

@@ -56,6 +56,7 @@ typedef struct cyaes_batcher_config {
     uint32_t max_batch_bytes; /* staging bytes per batch (0 => 32 MiB); caps a request */
     uint32_t max_delay_us;    /* longest a request waits for company (0 => 100 us)     */
     uint32_t inflight;        /* staging buffers / batches in flight (0 => 3)          */
+    uint32_t workers;         /* threads per gather / scatter of a batch (0 => 4)     */
 } cyaes_batcher_config;
 
 int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out);
@@ -80,6 +81,26 @@ int cyaes_batcher_submit_seal(cyaes_batcher* b, uint32_t slot, int32_t conn_id, 
  * (= 4 + packet_size); its payload is decrypted in place. */
 int cyaes_batcher_submit_open(cyaes_batcher* b, uint32_t slot, uint8_t* packet, uint32_t packet_bytes,
                               cyaes_done_fn done, void* user);
+
+/* Bulk submit: one call for all the requests a relay looper collected in one
+ * poll iteration (one shard lock for all of them).  Per request:
+ *   ENCRYPT / DECRYPT: in, out, size as cyaes_batcher_submit;
+ *   RELAY_SEAL: in = payload, size = chunk bytes, out = packet_out, conn_id;
+ *   RELAY_OPEN: out (or in) = packet, size = packet bytes.
+ * Invalid requests are skipped (their `done` is not called); status[i]
+ * (nullable) receives each request's code; returns the first error or
+ * CYAES_OK.  A thread's requests complete in its submission order. */
+typedef struct cyaes_batch_req {
+    int op;
+    uint32_t slot;
+    int32_t conn_id;
+    const uint8_t* in;
+    uint8_t* out;
+    uint32_t size;
+    cyaes_done_fn done;
+    void* user;
+} cyaes_batch_req;
+int cyaes_batcher_submit_many(cyaes_batcher* b, const cyaes_batch_req* reqs, uint32_t n, int* status);
 
 /* Blocks until every request submitted before the call has completed
  * (callbacks returned).  Returns the first error status seen since the

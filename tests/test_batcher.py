@@ -220,3 +220,76 @@ def test_update_keys_partial():
     for p, k in enumerate(table):
         assert got[256 * p:256 * (p + 1)] == bytes(oracle.Rijndael(k).encrypt(bytearray(src[256 * p:256 * (p + 1)])))
     ctx.close()
+
+
+def test_submit_many_mixed_ops_order_and_errors(batcher):
+    """cyaes_batcher_submit_many: ENCRYPT / DECRYPT / RELAY_SEAL / RELAY_OPEN in
+    one call from several threads; invalid entries are rejected individually
+    (status, no callback); each thread's requests complete in submission order."""
+    keys = _keys(3, 7)
+    slots = [batcher.session_open(k) for k in keys]
+    checks, lock = [], threading.Lock()
+
+    def worker(tid):
+        rng = random.Random(500 + tid)
+        order = []
+        for rnd in range(20):
+            reqs, recs = [], []
+            for i in range(rng.randrange(1, 40)):
+                k = rng.randrange(len(keys))
+                kind = rng.randrange(5)
+                rec = {"k": k, "kind": kind, "status": None, "seq": (rnd, i)}
+
+                def done(status, rec=rec):
+                    rec["status"] = status
+                    order.append(rec["seq"])
+                if kind <= 1:  # ENCRYPT / DECRYPT
+                    data = bytes(rng.randrange(256) for _ in range(16 * rng.randrange(0, 100)))
+                    rec.update(data=data, out=bytearray(len(data)))
+                    reqs.append((kind, slots[k], data, rec["out"], None, done, 0))
+                elif kind == 2:  # SEAL
+                    chunk = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 3000)))
+                    rec.update(chunk=chunk, conn=tid * 1000 + i, out=bytearray(ca.relay_packet_bytes(len(chunk))))
+                    reqs.append((ca.OP_RELAY_SEAL, slots[k], chunk, rec["out"], len(chunk), done, rec["conn"]))
+                elif kind == 3:  # OPEN
+                    chunk = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 3000)))
+                    sealed = ro.seal_forward(keys[k], 77, chunk)
+                    rec.update(chunk=chunk, sealed=sealed, out=bytearray(sealed))
+                    reqs.append((ca.OP_RELAY_OPEN, slots[k], None, rec["out"], len(sealed), done, 0))
+                else:  # invalid: size not a multiple of 16
+                    rec.update(out=bytearray(20))
+                    reqs.append((ca.OP_ENCRYPT, slots[k], bytes(20), rec["out"], 20, done, 0))
+                recs.append(rec)
+            st = batcher.submit_many(reqs)
+            for rec, s in zip(recs, st):
+                rec["submit"] = s
+            with lock:
+                checks.extend(recs)
+        with lock:
+            checks.append({"order": order})
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(3)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert batcher.flush() == ca.CYAES_OK
+    for rec in checks:
+        if "order" in rec:
+            assert rec["order"] == sorted(rec["order"])  # per-thread FIFO
+            continue
+        if rec["kind"] == 4:
+            assert rec["submit"] == ca.CYAES_EINVAL and rec["status"] is None
+            continue
+        assert rec["submit"] == ca.CYAES_OK and rec["status"] == ca.CYAES_OK
+        aes = oracle.Rijndael(keys[rec["k"]])
+        if rec["kind"] == 0:
+            assert bytes(rec["out"]) == bytes(aes.encrypt(bytearray(rec["data"])))
+        elif rec["kind"] == 1:
+            assert bytes(rec["out"]) == bytes(aes.decrypt(bytearray(rec["data"])))
+        elif rec["kind"] == 2:
+            assert bytes(rec["out"]) == ro.seal_forward(keys[rec["k"]], rec["conn"], rec["chunk"])
+        else:
+            assert bytes(rec["out"]) == ro.open_forward(keys[rec["k"]], rec["sealed"])[2]
+    for s in slots:
+        batcher.session_close(s)

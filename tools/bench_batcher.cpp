@@ -11,6 +11,7 @@
 //
 // usage: bench_batcher [--op seal|open|enc|dec] [--size B] [--threads T]
 //                      [--window W] [--seconds S] [--batch-mb M] [--delay-us D]
+//                      [--workers K] [--inflight I] [--bulk 0|1]
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -72,6 +73,19 @@ static int submit(Looper* L, Slot* s) {
     }
 }
 
+static cyaes_batch_req make_req(Looper* L, Slot* s) {
+    s->t0 = Clock::now();
+    switch (L->op) {
+        case CYAES_OP_RELAY_SEAL:
+            return {CYAES_OP_RELAY_SEAL, L->session, 7, s->in.data(), s->out.data(), L->size, on_done, s};
+        case CYAES_OP_RELAY_OPEN:
+            memcpy(s->out.data(), s->in.data(), s->in.size());
+            return {CYAES_OP_RELAY_OPEN, L->session, 0, nullptr, s->out.data(), (uint32_t)s->out.size(), on_done, s};
+        default:
+            return {L->op, L->session, 0, s->in.data(), s->out.data(), L->size, on_done, s};
+    }
+}
+
 static double pct(std::vector<double>& v, double p) {
     if (v.empty()) return 0;
     size_t k = std::min(v.size() - 1, (size_t)(p * (v.size() - 1)));
@@ -81,7 +95,7 @@ static double pct(std::vector<double>& v, double p) {
 
 int main(int argc, char** argv) {
     std::string op = "seal";
-    uint32_t size = 1472, threads = 8, window = 512, batch_mb = 32, delay_us = 100;
+    uint32_t size = 1472, threads = 8, window = 512, batch_mb = 32, delay_us = 100, workers = 0, inflight = 3, bulk = 1;
     double seconds = 5;
     for (int i = 1; i + 1 < argc; i += 2) {
         std::string a = argv[i];
@@ -92,13 +106,16 @@ int main(int argc, char** argv) {
         else if (a == "--seconds") seconds = atof(argv[i + 1]);
         else if (a == "--batch-mb") batch_mb = atoi(argv[i + 1]);
         else if (a == "--delay-us") delay_us = atoi(argv[i + 1]);
+        else if (a == "--workers") workers = atoi(argv[i + 1]);
+        else if (a == "--inflight") inflight = atoi(argv[i + 1]);
+        else if (a == "--bulk") bulk = atoi(argv[i + 1]);
     }
     const int opc = op == "seal" ? CYAES_OP_RELAY_SEAL : op == "open" ? CYAES_OP_RELAY_OPEN
                     : op == "dec" ? CYAES_OP_DECRYPT : CYAES_OP_ENCRYPT;
     if ((opc == CYAES_OP_ENCRYPT || opc == CYAES_OP_DECRYPT) && size % 16) size = cyaes_relay_round16(size);
     if (opc >= CYAES_OP_RELAY_SEAL && size > CYAES_RELAY_MAX_CHUNK) size = CYAES_RELAY_MAX_CHUNK;
 
-    cyaes_batcher_config cfg = {0, batch_mb << 20, delay_us, 3};
+    cyaes_batcher_config cfg = {0, batch_mb << 20, delay_us, inflight, workers};
     cyaes_batcher* b = nullptr;
     int st = cyaes_batcher_create(&cfg, &b);
     if (st) {
@@ -141,9 +158,10 @@ int main(int argc, char** argv) {
     const auto t0 = Clock::now();
     std::vector<std::thread> th;
     for (auto& L : loopers) {
-        th.emplace_back([&L, &stop] {
+        th.emplace_back([&L, &stop, bulk] {
             for (auto& s : L.slots) submit(&L, &s);
             std::vector<Slot*> again;
+            std::vector<cyaes_batch_req> reqs;
             while (!stop.load(std::memory_order_relaxed)) {
                 {
                     std::lock_guard<std::mutex> lk(L.mu);
@@ -153,7 +171,13 @@ int main(int argc, char** argv) {
                     std::this_thread::sleep_for(std::chrono::microseconds(20));
                     continue;
                 }
-                for (Slot* s : again) submit(&L, s);
+                if (bulk) {  // one cyaes_batcher_submit_many per poll, as a relay looper would
+                    reqs.clear();
+                    for (Slot* s : again) reqs.push_back(make_req(&L, s));
+                    cyaes_batcher_submit_many(L.b, reqs.data(), (uint32_t)reqs.size(), nullptr);
+                } else {
+                    for (Slot* s : again) submit(&L, s);
+                }
                 again.clear();
             }
         });
@@ -196,11 +220,12 @@ int main(int argc, char** argv) {
     const double sync_s = std::chrono::duration<double>(Clock::now() - s0).count();
 
     printf("{\"metric\": \"batcher %s requests/s host-to-host\", \"op\": \"%s\", \"size\": %u, \"threads\": %u, "
-           "\"window\": %u, \"batch_mb\": %u, \"delay_us\": %u, \"seconds\": %.2f, \"requests\": %llu, "
+           "\"window\": %u, \"batch_mb\": %u, \"delay_us\": %u, \"workers\": %u, \"inflight\": %u, \"bulk\": %u, "
+           "\"seconds\": %.2f, \"requests\": %llu, "
            "\"requests_per_s\": %.0f, \"payload_gibs\": %.3f, \"mean_batch\": %.1f, \"lat_p50_us\": %.0f, "
            "\"lat_p99_us\": %.0f, \"errors\": %d, \"sync_dropin_calls_per_s\": %.0f, "
            "\"sync_dropin_gibs\": %.4f}\n",
-           op.c_str(), op.c_str(), size, threads, window, batch_mb, delay_us, el, (unsigned long long)counted,
+           op.c_str(), op.c_str(), size, threads, window, batch_mb, delay_us, workers, inflight, bulk, el, (unsigned long long)counted,
            counted / el, counted * payload / el / (1u << 30), batches > 0 ? (st1[0] - st0[0]) / batches : 0.0, p50,
            p99, err, calls / sync_s, calls * (double)buf.size() / sync_s / (1u << 30));
     return err ? 2 : 0;
