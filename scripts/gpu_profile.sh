@@ -1,6 +1,7 @@
 #!/bin/bash
-# One GPU-box session: parity tests, bench (+cpu baseline), e2e bench,
-# rocprofv3 kernel-trace stats, PMC traffic passes.  Output: gpurun_out/$TAG/
+# One GPU-box session: parity tests, bench (+cpu baseline), the other configs,
+# end-to-end (host memory) bench and link probe, rocprofv3 kernel-trace stats,
+# PMC traffic passes.  Output: gpurun_out/$TAG/
 # usage: scripts/gpu_profile.sh TAG
 set -u
 TAG=${1:-run}
@@ -17,9 +18,14 @@ step() {  # step NAME SECONDS CMD...
   if [ $rc -ne 0 ]; then tail -5 "$O/$name.err"; exit $rc; fi
 }
 cd "$R"
-step pytest_gpu 600 python -m pytest tests -m gpu -q
+step pytest_gpu 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread
 step bench 400 python bench.py --steps 10 --warmup 2
-step bench_e2e 400 python bench_e2e.py --payloads 65536 --chunk-mib 1024 --streams 3
+step bench_B 200 python bench.py --config B --steps 20 --warmup 2 --no-cpu
+step bench_D 200 python bench.py --config D --steps 20 --warmup 2 --no-cpu
+step bench_A 200 python bench.py --config A --steps 20 --warmup 2 --no-cpu
+step linkprobe 200 python tools/linkprobe.py
+step bench_e2e_pinned 300 python bench_e2e.py --host pinned
+step bench_e2e_pageable 300 python bench_e2e.py --host pageable
 cd /tmp
 step rocprof_stats 400 rocprofv3 --kernel-trace --stats -d "$O/rocprof" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu
 step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" --steps 2 --warmup 0 --no-cpu --no-verify
