@@ -72,13 +72,14 @@ def session_keys(n):
     return b"".join(struct.pack("<QQ", sm(seed + 2 * s), sm(seed + 2 * s + 1)) for s in range(n))
 
 
-def cpu_baseline(cfg_name, npay, pb, ppk, d_ct, torch):
+def cpu_baseline(cfg_name, npay, pb, ppk, d_ct, torch, sample=0):
     """Oracle (scalar reference restatement) on the host cores; bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
-    sample = min(npay, int(max(1, (2 << 30) // pb)))  # ~2 GiB of payload
+    # ~4 GiB of payload by default: ~20 s of CPU work over 16 threads
+    sample = min(npay, sample if sample > 0 else int(max(1, (4 << 30) // pb)))
     keys = [bytes(range(16))] if not ppk else [session_keys(sample // ppk + 1)[16 * s:16 * s + 16]
                                               for s in range(sample // ppk + 1)]
     pt = oracle.synthetic(0, sample, pb)
@@ -247,7 +248,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         log("cpu baseline ...")
-        cpu = cpu_baseline(args.config, npay, pb, ppk, d_ct, torch)
+        cpu = cpu_baseline(args.config, npay, pb, ppk, d_ct, torch, args.cpu_sample)
 
     if rank == 0:
         out = {
