@@ -77,6 +77,9 @@ def test_argument_errors_without_device():
     assert lib.cyaes_key_expand(None, ctypes.byref(k)) == ca.CYAES_EINVAL
     assert lib.cyaes_gpu_encrypt_uniform(None, None, None, 1, 16, None, 0, None, None, None) == ca.CYAES_EINVAL
     assert lib.cyaes_gpu_fill_synthetic(None, 0, 1, 16, 0, None) == ca.CYAES_EINVAL
+    for fn in (lib.cyaes_gpu_encrypt_host, lib.cyaes_gpu_decrypt_host):
+        assert fn(None, buf, buf, 1, 16, 0, 0) == ca.CYAES_EINVAL
+    assert lib.cyaes_batcher_submit_many(None, None, 0, None) == ca.CYAES_EINVAL
 
 
 def _has_gpu():

@@ -86,3 +86,21 @@ def test_batcher_without_device_fails_loudly():
     with pytest.raises(ca.CyaesError) as e:
         ca.Batcher(0)
     assert e.value.status == ca.CYAES_ENODEV
+
+
+def test_relay_wire_format_fuzz_under_sanitizers(tmp_path):
+    """tests/cpp/fuzz_relay.cpp: random FORWARD / foreign / garbage / truncated
+    streams through the host parser and builder, built with ASan + UBSan."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "fuzz_relay")
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-I" + os.path.join(root, "include"), "-o", exe,
+                    os.path.join(root, "tests", "cpp", "fuzz_relay.cpp"),
+                    os.path.join(root, "cyclone_amd", "csrc", "cyaes_relay.cpp")], check=True)
+    # verify_asan_link_order=0: tolerate libraries preloaded by the environment
+    r = subprocess.run([exe, "3000"], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, ASAN_OPTIONS="verify_asan_link_order=0:detect_leaks=0"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "3000 streams ok" in r.stdout
