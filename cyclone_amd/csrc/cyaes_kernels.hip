@@ -10,16 +10,16 @@
 //    Tables and round keys are byte-swapped once on the host, so no swaps run
 //    on the device.
 //  * T-tables live in LDS as 256 rows x 256 B: row x holds A[x] replicated in
-//    32 slots and B[x] in the next 32.  A lookup address is one v_perm_b32,
-//    (x << 8) | (lane&31)*4, and lane l always hits bank l%32: the gathers are
-//    bank-conflict-free.  A second 64 KiB region is selected through byte 2 of
-//    the lane-offset register, still one v_perm_b32.
-//    Encrypt keeps all four T-tables (TL1|TL2, TL3|TL4): a column is
-//        xor3(TL1[b0], TL2[b1], xor3(TL3[b2], TL4[b3], k)).
-//    Decrypt fills the whole 160 KiB: TL5|TL6, TL7|TL8 and a 32 KiB Si image
-//    with 128-B rows (address = perm >> 1), so its columns have the same form.
-//    The last round's S-box bytes come from TL1/TL3 bytes (encrypt) or the
-//    Si x 0x01010101 image (decrypt), merged with v_bfi_b32 / v_perm_b32.
+//    32 slots and B[x] in the next 32.  A lookup address is (x << 8) |
+//    (lane&31)*4, and lane l always hits bank l%32: the gathers are
+//    bank-conflict-free.  The address is one v_perm_b32 (half-rate on gfx950),
+//    or for byte 1, already on the row bits, one full-rate v_bitop3_b32.  A
+//    second 64 KiB region is selected through byte 2 of the lane-offset
+//    register.  Both directions keep all four T-tables (T1|T3, T2|T4): a
+//    column is  xor3(T1[b0], T2[b1], xor3(T3[b2], T4[b3], k))  (tcol).
+//    Decrypt fills the whole 160 KiB: TL5|TL7, TL6|TL8 and a 32 KiB Si image
+//    with 128-B rows.  The last round's S-box bytes come from T-table bytes
+//    (encrypt) or the Si x 0x01010101 image (decrypt), merged with bitop3.
 //  * Round keys are wave-uniform and live in SGPRs (s_load from the key table;
 //    a per-payload key index is handled by a waterfall over the distinct keys
 //    present in a wave, normally one).
@@ -103,8 +103,6 @@ __device__ __forceinline__ uint32_t tcol(const char* lds, uint32_t lo, uint32_t 
     const uint32_t l3 = ld(lds + kHalfB, addr(x3, lo, region1(kSel3))); // T4[b3]
     return xor3(l0, l1, xor3(l2, l3, k));
 }
-#define ecol tcol
-#define dcol tcol
 
 // Merge the four last-round bytes (byte j of word j-th lookup).
 __device__ __forceinline__ uint32_t merge4(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3) {
@@ -123,36 +121,6 @@ __device__ __forceinline__ uint32_t enc_last(const char* lds, uint32_t lo, uint3
     const uint32_t l2 = ld(lds, addr(x2, lo, kSel2));            // TL1
     const uint32_t l3 = ld(lds, addr(x3, lo, region1(kSel3)));   // TL2
     return merge4(l0, l1, l2, l3);
-}
-
-// N independent states (N-way ILP): s = plaintext ^ chain ^ ek[0..3] on
-// entry, ciphertext on exit.
-template <int N>
-__device__ __forceinline__ void enc_blocks(const char* lds, uint32_t lo, const uint32_t* __restrict__ ek,
-                                           uint32_t (&s)[N][4]) {
-#pragma unroll
-    for (int r = 1; r < 10; r++) {
-        uint32_t t[N][4];
-#pragma unroll
-        for (int n = 0; n < N; n++) {
-            t[n][0] = ecol(lds, lo, s[n][0], s[n][1], s[n][2], s[n][3], ek[4 * r + 0]);
-            t[n][1] = ecol(lds, lo, s[n][1], s[n][2], s[n][3], s[n][0], ek[4 * r + 1]);
-            t[n][2] = ecol(lds, lo, s[n][2], s[n][3], s[n][0], s[n][1], ek[4 * r + 2]);
-            t[n][3] = ecol(lds, lo, s[n][3], s[n][0], s[n][1], s[n][2], ek[4 * r + 3]);
-        }
-#pragma unroll
-        for (int n = 0; n < N; n++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) s[n][j] = t[n][j];
-    }
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        const uint32_t o0 = enc_last(lds, lo, s[n][0], s[n][1], s[n][2], s[n][3]) ^ ek[40];
-        const uint32_t o1 = enc_last(lds, lo, s[n][1], s[n][2], s[n][3], s[n][0]) ^ ek[41];
-        const uint32_t o2 = enc_last(lds, lo, s[n][2], s[n][3], s[n][0], s[n][1]) ^ ek[42];
-        const uint32_t o3 = enc_last(lds, lo, s[n][3], s[n][0], s[n][1], s[n][2]) ^ ek[43];
-        s[n][0] = o0; s[n][1] = o1; s[n][2] = o2; s[n][3] = o3;
-    }
 }
 
 #if CYAES_VALU_FILLER
@@ -182,10 +150,10 @@ __device__ __forceinline__ void enc_block(const char* lds, uint32_t lo, const ui
 #endif
 #pragma unroll
     for (int r = 1; r < 10; r++) {
-        const uint32_t a0 = ecol(lds, lo, s0, s1, s2, s3, ek[4 * r + 0]);
-        const uint32_t a1 = ecol(lds, lo, s1, s2, s3, s0, ek[4 * r + 1]);
-        const uint32_t a2 = ecol(lds, lo, s2, s3, s0, s1, ek[4 * r + 2]);
-        const uint32_t a3 = ecol(lds, lo, s3, s0, s1, s2, ek[4 * r + 3]);
+        const uint32_t a0 = tcol(lds, lo, s0, s1, s2, s3, ek[4 * r + 0]);
+        const uint32_t a1 = tcol(lds, lo, s1, s2, s3, s0, ek[4 * r + 1]);
+        const uint32_t a2 = tcol(lds, lo, s2, s3, s0, s1, ek[4 * r + 2]);
+        const uint32_t a3 = tcol(lds, lo, s3, s0, s1, s2, ek[4 * r + 3]);
         FILLER_RUN(s0, s2);
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     }
@@ -259,10 +227,10 @@ __device__ __forceinline__ void dec_cbc(const char* lds, uint32_t lo, const uint
         uint32_t t[N][4];
 #pragma unroll
         for (int n = 0; n < N; n++) {
-            t[n][0] = dcol(lds, lo, s[n][0], s[n][3], s[n][2], s[n][1], dk[4 * r + 0]);
-            t[n][1] = dcol(lds, lo, s[n][1], s[n][0], s[n][3], s[n][2], dk[4 * r + 1]);
-            t[n][2] = dcol(lds, lo, s[n][2], s[n][1], s[n][0], s[n][3], dk[4 * r + 2]);
-            t[n][3] = dcol(lds, lo, s[n][3], s[n][2], s[n][1], s[n][0], dk[4 * r + 3]);
+            t[n][0] = tcol(lds, lo, s[n][0], s[n][3], s[n][2], s[n][1], dk[4 * r + 0]);
+            t[n][1] = tcol(lds, lo, s[n][1], s[n][0], s[n][3], s[n][2], dk[4 * r + 1]);
+            t[n][2] = tcol(lds, lo, s[n][2], s[n][1], s[n][0], s[n][3], dk[4 * r + 2]);
+            t[n][3] = tcol(lds, lo, s[n][3], s[n][2], s[n][1], s[n][0], dk[4 * r + 3]);
         }
 #pragma unroll
         for (int n = 0; n < N; n++)
