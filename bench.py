@@ -14,6 +14,11 @@ broadcasts it over RCCL (xGMI); every rank expands it on its device and
 processes its own payload shard (weak scaling: per-GPU batch fixed, payload
 indices [rank*P, (rank+1)*P) of the global stream).  No data-path collective.
 
+packet_configs: the north star's other named sizes, measured after the
+headline config at the same GPU count with the same timing rules: config B
+(1 M x 1,472 B, MTU-sized) and config D (4,096 session keys x 256 x 1,472 B).
+Reported beside `value`, never as it.
+
 cpu_baseline: the oracle (a plain-C restatement of the reference's scalar
 Rijndael, oracle/aes_oracle.c) timed on this host's cores on a bounded
 sample of the same workload, rank 0 at N=1 only.
@@ -56,6 +61,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=0, help="cpu baseline sample payloads (0 = auto)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--packet-configs", default="B,D",
+                    help="other BASELINE.json packet configs measured after the headline one ('none' to skip)")
+    ap.add_argument("--packet-steps", type=int, default=20)
     return ap.parse_args()
 
 
@@ -135,101 +143,114 @@ def main():
             dist.init_process_group(backend)
 
     import cyclone_amd as ca
-
-    npay, pb, ppk = CONFIGS[args.config]
-    if args.payloads:
-        npay = args.payloads
-    nbytes = npay * pb
-    stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
-
     from cyclone_amd import dist as cdist
 
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
     ctx = ca.GpuContext(device)
-    # Session key(s): rank 0 owns them (the relay's DH secret), RCCL-broadcast
-    # over xGMI straight into device memory; each GPU expands its own sessions.
-    p0, npay = cdist.weak_shard(npay, rank)
-    nkeys = cdist.session_range(0, npay * world, ppk)[1]
-    d_keys = cdist.broadcast_keys((session_keys(nkeys) if ppk else bytes(range(16))) if rank == 0 else None,
-                                  nkeys, "cuda")
-    k0, nk = cdist.session_range(p0, npay, ppk)
-    d_keys = d_keys[16 * k0: 16 * (k0 + nk)].contiguous()
-    ctx.set_keys_device(d_keys, nk, sh)
-
-    log("rank %d/%d: config %s, %d payloads x %d B = %.2f GiB per GPU, %d CUs"
-        % (rank, world, args.config, npay, pb, nbytes / 2**30, ctx.num_cus))
-    d_pt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    d_ct = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    d_rt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    ctx.fill_synthetic(d_pt, p0, npay, pb, PLAINTEXT_SEED, sh)
-
-    def enc():
-        ctx.encrypt_uniform(d_pt, d_ct, npay, pb, payloads_per_key=ppk, stream=sh)
-
-    def dec():
-        ctx.decrypt_uniform(d_ct, d_rt, npay, pb, payloads_per_key=ppk, stream=sh)
-
-    for _ in range(args.warmup):
-        enc()
-        dec()
-    torch.cuda.synchronize()
-
-    parity = None
-    if not args.no_verify:
-        golden = json.load(open(os.path.join(ROOT, "tests", "golden", "openssl_vectors.json")))["configs"]
-        gname = {"C": "C", "B": "B", "D": "D", "A": "A"}[args.config] if rank == 0 else (
-            "E_rank1" if (rank == 1 and args.config == "C") else None)
-        dp = ctx.digest(d_pt, nbytes, sh)
-        dc = ctx.digest(d_ct, nbytes, sh)
-        dr = ctx.digest(d_rt, nbytes, sh)
-        ok = dr == dp
-        g = golden.get(gname) if gname else None
-        if g and g["npayloads"] == npay and g["payload_bytes"] == pb and g["p0"] == p0:
-            ok = ok and ["%016x" % v for v in dc] == g["cipher_digest"] and ["%016x" % v for v in dp] == g["plain_digest"]
-        ok = ok and ctx.check() == ca.CYAES_OK
-        flag = torch.tensor([0 if ok else 1], device="cuda")
-        if world > 1:
-            dist.all_reduce(flag)
-        parity = "bit-exact" if int(flag.item()) == 0 else "MISMATCH"
-        log("parity:", parity)
-
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        enc()
-        ev[i][1].record(stream)
-        dec()
-        ev[i][2].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    t = float(elapsed.item())
-
-    enc_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps
-    dec_ms = sum(b.elapsed_time(c) for _, b, c in ev) / args.steps
+    golden = json.load(open(os.path.join(ROOT, "tests", "golden", "openssl_vectors.json")))["configs"]
     gib = float(1 << 30)
-    value = 2.0 * nbytes * args.steps * world / t / gib
 
-    def roof(ms):
-        ach = 2.0 * nbytes / (ms / 1e3) / 1e9  # algorithmic: read N + write N per launch
+    def run_config(name, npay, steps, warmup, verify, keep_cipher=False):
+        """One config, timed as the contract says; returns a result dict (rank-local
+        kernel times, max-over-ranks wall time)."""
+        _, pb, ppk = CONFIGS[name]
+        nbytes = npay * pb
+        # Session key(s): rank 0 owns them (the relay's DH secret), RCCL-broadcast
+        # over xGMI straight into device memory; each GPU expands its own sessions.
+        p0, npay = cdist.weak_shard(npay, rank)
+        nkeys = cdist.session_range(0, npay * world, ppk)[1]
+        d_keys = cdist.broadcast_keys((session_keys(nkeys) if ppk else bytes(range(16))) if rank == 0 else None,
+                                      nkeys, "cuda")
+        k0, nk = cdist.session_range(p0, npay, ppk)
+        d_keys = d_keys[16 * k0: 16 * (k0 + nk)].contiguous()
+        ctx.set_keys_device(d_keys, nk, sh)
+
+        log("rank %d/%d: config %s, %d payloads x %d B = %.2f GiB per GPU, %d CUs"
+            % (rank, world, name, npay, pb, nbytes / 2**30, ctx.num_cus))
+        d_pt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        d_ct = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        d_rt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        ctx.fill_synthetic(d_pt, p0, npay, pb, PLAINTEXT_SEED, sh)
+
+        def enc():
+            ctx.encrypt_uniform(d_pt, d_ct, npay, pb, payloads_per_key=ppk, stream=sh)
+
+        def dec():
+            ctx.decrypt_uniform(d_ct, d_rt, npay, pb, payloads_per_key=ppk, stream=sh)
+
+        for _ in range(warmup):
+            enc()
+            dec()
+        torch.cuda.synchronize()
+
+        parity = None
+        if verify:
+            gname = name if rank == 0 else ("E_rank1" if (rank == 1 and name == "C") else None)
+            dp = ctx.digest(d_pt, nbytes, sh)
+            dc = ctx.digest(d_ct, nbytes, sh)
+            dr = ctx.digest(d_rt, nbytes, sh)
+            ok = dr == dp
+            g = golden.get(gname) if gname else None
+            if g and g["npayloads"] == npay and g["payload_bytes"] == pb and g["p0"] == p0:
+                ok = ok and ["%016x" % v for v in dc] == g["cipher_digest"] and \
+                    ["%016x" % v for v in dp] == g["plain_digest"]
+            ok = ok and ctx.check() == ca.CYAES_OK
+            flag = torch.tensor([0 if ok else 1], device="cuda")
+            if world > 1:
+                dist.all_reduce(flag)
+            parity = "bit-exact" if int(flag.item()) == 0 else "MISMATCH"
+            log("config %s parity: %s" % (name, parity))
+
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+               torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            ev[i][0].record(stream)
+            enc()
+            ev[i][1].record(stream)
+            dec()
+            ev[i][2].record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        t = float(elapsed.item())
+        res = {
+            "name": name, "npay": npay, "pb": pb, "ppk": ppk, "nbytes": nbytes, "t": t, "steps": steps,
+            "value": 2.0 * nbytes * steps * world / t / gib,
+            "enc_ms": sum(a.elapsed_time(b) for a, b, _ in ev) / steps,
+            "dec_ms": sum(b.elapsed_time(c) for _, b, c in ev) / steps,
+            "parity": parity, "d_ct": d_ct if keep_cipher else None,
+        }
+        del d_pt, d_rt
+        if not keep_cipher:
+            del d_ct
+        return res
+
+    npay = args.payloads or CONFIGS[args.config][0]
+    main_res = run_config(args.config, npay, args.steps, args.warmup, not args.no_verify, keep_cipher=True)
+    nbytes, pb, ppk = main_res["nbytes"], main_res["pb"], main_res["ppk"]
+    npay, t, value = main_res["npay"], main_res["t"], main_res["value"]
+    enc_ms, dec_ms, parity = main_res["enc_ms"], main_res["dec_ms"], main_res["parity"]
+
+    def roof(ms, nb=nbytes):
+        ach = 2.0 * nb / (ms / 1e3) / 1e9  # algorithmic: read N + write N per launch
         return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4)}
 
-    def lds(ms):
+    def lds(ms, nb=nbytes):
         # The binding on-chip resource (DESIGN.md §3.4): 160 conflict-free ds_read_b32
         # lookups per 16-B block; nominal LDS rate 32 lanes/clk/CU (2 cycles per wave64
         # ds_read_b32), here priced at the 2.4 GHz peak shader clock.  In-kernel clock
         # probes (tools/ab.py + CYAES_CLOCK_PROBE) show ~1.9 GHz under this load.
-        look = LOOKUPS_PER_BLOCK * (nbytes / 16) / (ms / 1e3)
+        look = LOOKUPS_PER_BLOCK * (nb / 16) / (ms / 1e3)
         peak = LDS_LANES_PER_CLK_CU * NUM_CUS * 2.4e9
         return {"lookups_per_s": float("%.4g" % look), "peak_at_2p4ghz": float("%.4g" % peak),
                 "frac": round(look / peak, 4)}
@@ -248,7 +269,26 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         log("cpu baseline ...")
-        cpu = cpu_baseline(args.config, npay, pb, ppk, d_ct, torch, args.cpu_sample)
+        cpu = cpu_baseline(args.config, npay, pb, ppk, main_res["d_ct"], torch, args.cpu_sample)
+    main_res["d_ct"] = None
+    torch.cuda.empty_cache()
+
+    # The north star's other named packet sizes, at the same GPU count: MTU-sized
+    # payloads (config B) and per-session keys (config D).  Reported beside the
+    # headline config, never as `value`.
+    packet_configs = {}
+    for name in ([] if args.packet_configs == "none" else args.packet_configs.split(",")):
+        if name == args.config or name not in CONFIGS:
+            continue
+        r = run_config(name, CONFIGS[name][0], args.packet_steps, 2, not args.no_verify)
+        packet_configs[name] = {
+            "value": round(r["value"], 2), "unit": "GiB/s", "ms_per_step": round(r["t"] / r["steps"] * 1e3, 4),
+            "steps": r["steps"], "payloads_per_gpu": r["npay"], "payload_bytes": r["pb"],
+            "payloads_per_key": r["ppk"], "encrypt_ms": round(r["enc_ms"], 4), "decrypt_ms": round(r["dec_ms"], 4),
+            "hbm_frac_step": round(4.0 * r["nbytes"] / (r["t"] / r["steps"]) / 1e9 / HBM_PEAK_GBS, 4),
+            "parity": r["parity"],
+        }
+        torch.cuda.empty_cache()
 
     if rank == 0:
         out = {
@@ -263,6 +303,7 @@ def main():
                        "RCCL key broadcast" % world},
             "hbm_frac_step": round(4.0 * nbytes * world / (t / args.steps) / 1e9 / (HBM_PEAK_GBS * world), 4),
             "roofline": roofline, "kernels": kern, "cpu_baseline": cpu, "parity": parity,
+            "packet_configs": packet_configs,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
