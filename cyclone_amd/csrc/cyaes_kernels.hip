@@ -33,6 +33,13 @@
 //    (prio_feedback), so none runs a starved tail.
 #include "cyaes_internal.h"
 
+#ifndef CYAES_NO_PREFETCH
+#define CYAES_NO_PREFETCH 0    // A/B only: load each encrypt chunk at its top instead of one chunk ahead
+#endif
+#ifndef CYAES_TAIL_PREFETCH
+#define CYAES_TAIL_PREFETCH 1  // encrypt: prefetch a payload's partial last chunk with the chunk before
+#endif
+
 namespace cyaes {
 namespace {
 
@@ -181,8 +188,8 @@ __device__ __forceinline__ uint32_t dec_lo(uint32_t tid) { return ((tid & 31u) <
 constexpr uint32_t kSiRowMask = 0x00007F80u;
 template <int K>  // byte K of u
 __device__ __forceinline__ uint32_t addr_si(uint32_t u, uint32_t lsi) {
-    const uint32_t r = K == 0 ? u << 7 : u >> (8 * K - 7);
-    return sel(kSiRowMask, r, lsi);
+    if constexpr (K == 0) return sel(kSiRowMask, u << 7, lsi);
+    else return sel(kSiRowMask, u >> (8 * K - 7), lsi);
 }
 __device__ __forceinline__ uint32_t dec_last(const char* lds, uint32_t lsi, uint32_t x0, uint32_t x1, uint32_t x2,
                                              uint32_t x3) {
@@ -411,13 +418,19 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
 #pragma unroll
                     for (int j = 0; j < 8; j++) b[j] = ldb<RAGGED>(src, j);
                 }
+                bool have_tail = false;  // b[0, nb - i) already hold the last partial chunk
                 for (; i + 8 <= nb; i += 8) {
+                    const bool more = i + 16 <= nb;
+                    const bool tail = CYAES_TAIL_PREFETCH && !CYAES_NO_PREFETCH && !more && i + 8 < nb;  // partial last chunk
 #if !CYAES_NO_PREFETCH  // A/B: -8% encrypt time vs loading at the top of the chunk
                     uint4 bn[8];  // next chunk's loads in flight during this chunk's rounds
-                    const bool more = i + 16 <= nb;
                     if (more) {
 #pragma unroll
                         for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(src, i + 8 + j);
+                    } else if (tail) {
+#pragma unroll
+                        for (int j = 0; j < 7; j++)
+                            if (i + 8 + j < nb) bn[j] = ldb<RAGGED>(src, i + 8 + j);
                     }
 #endif
                     prio_feedback(&lead, ++prog, kEncPrioDiv);
@@ -432,19 +445,22 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
 #pragma unroll
                     for (int j = 0; j < 8; j++) stb<RAGGED>(dst, i + j, b[j]);  // (nt stores measured 3.6x slower)
 #if CYAES_NO_PREFETCH
-                    if (i + 16 <= nb) {
+                    if (more) {
 #pragma unroll
                         for (int j = 0; j < 8; j++) b[j] = ldb<RAGGED>(src, i + 8 + j);
                     }
 #else
-                    if (more) {
+                    if (more || tail) {
 #pragma unroll
                         for (int j = 0; j < 8; j++) b[j] = bn[j];
                     }
+                    have_tail = tail;
 #endif
                 }
-                for (; i < nb; i++) {
-                    const uint4 v = ldb<RAGGED>(src, i);
+                for (; i < nb; i++) {  // partial last chunk: from b (prefetched) or loaded here
+                    const uint4 v = have_tail ? b[0] : ldb<RAGGED>(src, i);
+#pragma unroll
+                    for (int j = 0; j < 7; j++) b[j] = b[j + 1];
                     uint32_t s0 = xor3(c.x, v.x, ek[0]), s1 = xor3(c.y, v.y, ek[1]);
                     uint32_t s2 = xor3(c.z, v.z, ek[2]), s3 = xor3(c.w, v.w, ek[3]);
                     enc_block(lds, lo, ek, s0, s1, s2, s3);
