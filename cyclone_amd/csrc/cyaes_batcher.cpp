@@ -21,6 +21,8 @@
 // A SEAL/OPEN request keeps its packet at data offset o + 4 so the payload
 // (packet offset 12) sits at o + 16.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -162,15 +164,33 @@ constexpr int kShards = 16;
 struct alignas(64) Shard {
     std::mutex mu;
     std::vector<Req> q;
+    uint64_t bytes = 0;     // data bytes queued in q
+    uint64_t enqueued = 0;  // requests ever enqueued here (flush target, stats)
 };
 int my_shard() {
     static std::atomic<int> next{0};
     thread_local int s = next.fetch_add(1) % kShards;
     return s;
 }
+// Per-thread snapshot of a batcher's session table, refreshed when the table's
+// version changes (open/close), so a submit takes no shared lock.
+std::atomic<uint64_t> g_batcher_ids{1};
+struct SessionSnap {
+    uint64_t batcher = 0, version = 0;
+    std::vector<std::shared_ptr<const Sched>> s;
+};
+thread_local SessionSnap t_snap;
+
 int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
 }
+
+// Per-thread phase times (ns), written only by their own thread, printed by
+// cyaes_batcher_destroy when CYAES_BATCHER_PROFILE is set (after the joins).
+struct Phases {
+    int64_t wait = 0, take = 0, form = 0, layout = 0, gather = 0, submit = 0;  // builder
+    int64_t sync = 0, scatter = 0, callbacks = 0, batches = 0, reqs = 0;       // completer
+};
 
 }  // namespace
 
@@ -184,7 +204,6 @@ struct cyaes_batcher {
     std::array<Shard, kShards> shards;
     std::atomic<int64_t> queued_reqs{0}, queued_bytes{0};  // transiently negative while a drain races an enqueue
     std::atomic<int64_t> oldest_ns{0};  // submit time of the oldest queued request (0: none recorded)
-    std::atomic<uint64_t> submitted{0};
     std::atomic<int> flushers{0};
     std::atomic<bool> stop{false};
 
@@ -200,9 +219,20 @@ struct cyaes_batcher {
 
     std::mutex smu;  // session table
     std::vector<std::shared_ptr<const Sched>> sessions;  // nullptr = free slot
+    std::atomic<uint64_t> sessions_version{1};
+    const uint64_t id = g_batcher_ids.fetch_add(1);
+    const SessionSnap& snapshot();
+    uint64_t enqueued_total();
 
     std::unique_ptr<Pool> gather_pool, scatter_pool;
     std::thread builder, completer;
+    Phases pb, pc;  // builder / completer phase times
+    struct Lists {  // builder-private scratch of launch(), reused across batches
+        std::vector<uint64_t> eo, doff, o2;
+        std::vector<uint32_t> el, ek, dl, dk, l2, k2, at;
+        std::unordered_map<const Sched*, uint32_t> kidx;
+        std::vector<const Sched*> klist;
+    } lists;
 
     // Cost of a request in a stage: data + meta (16 B) + a schedule if its key is new to the batch.
     static uint64_t cost(const Req& r) { return r.data_bytes() + 16; }
@@ -210,16 +240,18 @@ struct cyaes_batcher {
     void build_loop();
     void complete_loop();
     int launch(Stage* st);
-    int make(const cyaes_batch_req& q, Req* r);
+    int make(const cyaes_batch_req& q, const SessionSnap& ss, Req* r);
     void enqueue(Req* rs, size_t n, uint64_t nbytes);
 };
 
 void cyaes_batcher::build_loop() {
     std::vector<Req> carry;  // builder-private: taken from the shards, not yet batched (older than the shards)
     size_t cpos = 0;
+    std::array<std::vector<Req>, kShards> spare;  // swapped into the shards: their capacity is recycled
     std::unordered_map<const Sched*, int> seen;
     for (;;) {
         Stage* st = nullptr;
+        const int64_t tw = now_ns();
         {
             std::unique_lock<std::mutex> lk(mu);
             if (cpos == carry.size()) {
@@ -239,41 +271,69 @@ void cyaes_batcher::build_loop() {
             st = free_stages.back();
             free_stages.pop_back();
         }
-        // Take every shard's queue (a swap under each shard lock).
+        const int64_t tt = now_ns();
+        pb.wait += tt - tw;
+        // Take every shard's queue: a swap with a spare (empty, with capacity)
+        // under each shard lock, then one move per request into carry.
         oldest_ns.store(0);
         int64_t took = 0, took_bytes = 0;
-        for (Shard& sh : shards) {
-            std::vector<Req> q;
+        for (int i = 0; i < kShards; i++) {
+            Shard& sh = shards[i];
             {
                 std::lock_guard<std::mutex> lk(sh.mu);
-                q.swap(sh.q);
+                if (sh.q.empty()) continue;
+                sh.q.swap(spare[i]);
+                took_bytes += (int64_t)sh.bytes;
+                sh.bytes = 0;
             }
-            for (const Req& r : q) took_bytes += r.data_bytes();
+            std::vector<Req>& q = spare[i];
             took += (int64_t)q.size();
-            if (carry.empty()) carry.swap(q);
+            if (cpos == carry.size()) {
+                carry.clear();
+                cpos = 0;
+            }
+            if (carry.empty()) carry.swap(q);  // q now holds carry's old (empty) buffer
             else carry.insert(carry.end(), std::make_move_iterator(q.begin()), std::make_move_iterator(q.end()));
+            q.clear();
         }
         queued_reqs.fetch_sub(took);
         queued_bytes.fetch_sub(took_bytes);
+        const int64_t tf = now_ns();
+        pb.take += tf - tt;
+        // Cut the batch: [cpos, end) of carry, bounded by max_batch_bytes and the stage.
         st->reqs.clear();
         uint64_t used = 0, data = 0;
         seen.clear();
-        for (; cpos < carry.size(); cpos++) {
-            Req& r = carry[cpos];
-            const bool new_key = !seen.count(r.key.get());
-            const uint64_t c = cost(r) + (new_key ? sizeof(Sched) : 0);
-            if (!st->reqs.empty() && (data + r.data_bytes() > cfg.max_batch_bytes || used + c + 64 > stage_cap))
-                break;
-            if (new_key) seen.emplace(r.key.get(), 0);
+        const Sched* last = nullptr;
+        size_t end = cpos;
+        for (; end < carry.size(); end++) {
+            const Req& r = carry[end];
+            bool new_key = false;
+            if (r.key.get() != last) {
+                last = r.key.get();
+                new_key = seen.emplace(last, 0).second;
+            }
+            const uint64_t db = r.data_bytes();
+            const uint64_t c = db + 16 + (new_key ? sizeof(Sched) : 0);
+            if (end > cpos && (data + db > cfg.max_batch_bytes || used + c + 64 > stage_cap)) break;
             used += c;
-            data += r.data_bytes();
-            st->reqs.push_back(std::move(r));
+            data += db;
+        }
+        if (cpos == 0 && end == carry.size()) {
+            st->reqs.swap(carry);  // the whole carry: no moves (carry takes the stage's old buffer)
+            carry.clear();
+            cpos = 0;
+        } else {
+            st->reqs.insert(st->reqs.end(), std::make_move_iterator(carry.begin() + cpos),
+                            std::make_move_iterator(carry.begin() + end));
+            cpos = end;
         }
         if (st->reqs.empty()) {  // raced: nothing taken (cannot happen with took > 0 or carry)
             std::lock_guard<std::mutex> lk(mu);
             free_stages.push_back(st);
             continue;
         }
+        pb.form += now_ns() - tf;
         st->status = launch(st);
         std::lock_guard<std::mutex> lk(mu);
         inflight.push_back(st);
@@ -286,13 +346,21 @@ void cyaes_batcher::build_loop() {
 
 // Gathers st->reqs into the stage and launches the batch on its stream.
 int cyaes_batcher::launch(Stage* st) {
+    const int64_t t0 = now_ns();
     const size_t n = st->reqs.size();
     st->off.resize(n);
     // Data section + per-direction lists.
-    std::vector<uint64_t> eo, doff;
-    std::vector<uint32_t> el, ek, dl, dk;
-    std::unordered_map<const Sched*, uint32_t> kidx;
-    std::vector<const Sched*> klist;
+    std::vector<uint64_t>& eo = lists.eo;
+    std::vector<uint64_t>& doff = lists.doff;
+    std::vector<uint32_t>&el = lists.el, &ek = lists.ek, &dl = lists.dl, &dk = lists.dk;
+    for (auto* v : {&eo, &doff}) v->clear(), v->reserve(n);
+    for (auto* v : {&el, &ek, &dl, &dk}) v->clear(), v->reserve(n);
+    std::unordered_map<const Sched*, uint32_t>& kidx = lists.kidx;
+    std::vector<const Sched*>& klist = lists.klist;
+    kidx.clear();
+    klist.clear();
+    const Sched* last = nullptr;
+    uint32_t k = 0;
     uint64_t pos = 0;
     for (size_t i = 0; i < n; i++) {  // layout pass (the copies run below, in parallel)
         const Req& r = st->reqs[i];
@@ -300,14 +368,16 @@ int cyaes_batcher::launch(Stage* st) {
         const uint64_t coff = r.op >= CYAES_OP_RELAY_SEAL ? pos + 16 : pos;  // where the kernel works
         pos += r.data_bytes();
         if (r.crypt == 0) continue;  // size 0: a no-op (cyr_rijndael.cpp:600 loop never runs)
-        auto it = kidx.find(r.key.get());
-        uint32_t k;
-        if (it == kidx.end()) {
-            k = (uint32_t)klist.size();
-            kidx.emplace(r.key.get(), k);
-            klist.push_back(r.key.get());
-        } else {
-            k = it->second;
+        if (r.key.get() != last) {  // requests come in per-thread runs: hash only on a change
+            last = r.key.get();
+            auto it = kidx.find(last);
+            if (it == kidx.end()) {
+                k = (uint32_t)klist.size();
+                kidx.emplace(last, k);
+                klist.push_back(last);
+            } else {
+                k = it->second;
+            }
         }
         const bool dec = r.op == CYAES_OP_DECRYPT || r.op == CYAES_OP_RELAY_OPEN;
         (dec ? doff : eo).push_back(coff);
@@ -315,6 +385,8 @@ int cyaes_batcher::launch(Stage* st) {
         (dec ? dk : ek).push_back(k);
     }
     st->data_end = pos;
+    const int64_t t1 = now_ns();
+    pb.layout += t1 - t0;
     gather_pool->run(n, kCopyChunk, [st](size_t b, size_t e) {
         for (size_t i = b; i < e; i++) {
             const Req& r = st->reqs[i];
@@ -333,17 +405,26 @@ int cyaes_batcher::launch(Stage* st) {
             }
         }
     });
+    const int64_t t2 = now_ns();
+    pb.gather += t2 - t1;
     // Encrypt runs one chain per lane and waterfalls over the distinct keys of
     // a wave (cyaes_kernels.hip, k_encrypt), so order its list by key: a wave
     // then sees one key, two at a boundary, instead of one per looper thread.
     // (Decrypt runs one payload per wave: one key per wave already.)
     if (klist.size() > 1 && !eo.empty()) {
-        std::vector<uint32_t> ord(eo.size());
-        for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
-        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return ek[x] < ek[y]; });
-        std::vector<uint64_t> o2(eo.size());
-        std::vector<uint32_t> l2(el.size()), k2(ek.size());
-        for (size_t i = 0; i < ord.size(); i++) o2[i] = eo[ord[i]], l2[i] = el[ord[i]], k2[i] = ek[ord[i]];
+        // Stable counting sort by key index (key indices are dense: 0..klist.size()-1).
+        std::vector<uint64_t>& o2 = lists.o2;
+        std::vector<uint32_t>&l2 = lists.l2, &k2 = lists.k2, &at = lists.at;
+        o2.resize(eo.size());
+        l2.resize(el.size());
+        k2.resize(ek.size());
+        at.assign(klist.size() + 1, 0);
+        for (uint32_t x : ek) at[x + 1]++;
+        for (size_t j = 1; j < at.size(); j++) at[j] += at[j - 1];
+        for (size_t i = 0; i < ek.size(); i++) {
+            const uint32_t d = at[ek[i]]++;
+            o2[d] = eo[i], l2[d] = el[i], k2[d] = ek[i];
+        }
         // Small batch: start every key group on a wave boundary with empty
         // (0-byte) lanes, so no wave waterfalls; the waves are then all
         // latency-bound chains on separate CUs (A/B on bench_batcher seal 1472 B).
@@ -398,7 +479,26 @@ int cyaes_batcher::launch(Stage* st) {
     if (rc != CYAES_OK) return rc;
     e = hipMemcpyAsync(st->h, st->d, st->data_end, hipMemcpyDeviceToHost, st->stream);
     if (e == hipSuccess) e = hipEventRecord(st->done, st->stream);
+    pb.submit += now_ns() - t2;
     return map_err(e);
+}
+
+// Copies request i's result out of the stage into the caller's buffer.
+static void scatter(Stage* st, size_t i) {
+    const Req& r = st->reqs[i];
+    const uint8_t* src = st->h + st->off[i];
+    switch (r.op) {
+        case CYAES_OP_ENCRYPT:
+        case CYAES_OP_DECRYPT:
+            memcpy(r.out, src, r.size);
+            break;
+        case CYAES_OP_RELAY_SEAL:
+            memcpy(r.out, src + 4, CYAES_RELAY_PAYLOAD_OFFSET + r.crypt);
+            break;
+        case CYAES_OP_RELAY_OPEN:  // header untouched, payload decrypted in place
+            memcpy(r.out + CYAES_RELAY_PAYLOAD_OFFSET, src + 16, r.crypt);
+            break;
+    }
 }
 
 void cyaes_batcher::complete_loop() {
@@ -410,34 +510,30 @@ void cyaes_batcher::complete_loop() {
         inflight.pop_front();
         lk.unlock();
         int status = st->status;
+        const int64_t t0 = now_ns();
         if (status == CYAES_OK) status = map_err(hipEventSynchronize(st->done));
-        if (status == CYAES_OK) {
+        const int64_t t1 = now_ns();
+        pc.sync += t1 - t0;
+        if (status == CYAES_OK)
             scatter_pool->run(st->reqs.size(), kCopyChunk, [st](size_t b, size_t e) {
-                for (size_t i = b; i < e; i++) {
-                    const Req& r = st->reqs[i];
-                    const uint8_t* src = st->h + st->off[i];
-                    switch (r.op) {
-                        case CYAES_OP_ENCRYPT:
-                        case CYAES_OP_DECRYPT:
-                            memcpy(r.out, src, r.size);
-                            break;
-                        case CYAES_OP_RELAY_SEAL:
-                            memcpy(r.out, src + 4, CYAES_RELAY_PAYLOAD_OFFSET + r.crypt);
-                            break;
-                        case CYAES_OP_RELAY_OPEN:  // header untouched, payload decrypted in place
-                            memcpy(r.out + CYAES_RELAY_PAYLOAD_OFFSET, src + 16, r.crypt);
-                            break;
-                    }
-                }
+                for (size_t i = b; i < e; i++) scatter(st, i);
             });
-        }
+        const int64_t t2 = now_ns();
+        pc.scatter += t2 - t1;
+        // Callbacks on this thread, in batch order.  (A/B: spreading them over
+        // the scatter workers by submission shard was slower under the
+        // relay-shaped load of tools/bench_batcher.cpp: the callbacks then
+        // contend with the submitting threads.)
         uint64_t nbytes = 0;
-        for (const Req& r : st->reqs) {  // callbacks in batch order, on this thread
+        for (const Req& r : st->reqs) {
             nbytes += r.crypt;
             if (r.done) r.done(r.user, status);
         }
         const size_t nreq = st->reqs.size();
         st->reqs.clear();  // drops the schedule references
+        pc.callbacks += now_ns() - t2;
+        pc.batches++;
+        pc.reqs += (int64_t)nreq;
         lk.lock();
         completed += nreq;
         batches++;
@@ -453,8 +549,31 @@ void cyaes_batcher::complete_loop() {
     }
 }
 
-// Validates one request and pins its session's schedule (caller holds smu).
-int cyaes_batcher::make(const cyaes_batch_req& q, Req* r) {
+// This thread's snapshot of the session table (refreshed under smu when an
+// open/close has bumped the version since this thread last looked).
+const SessionSnap& cyaes_batcher::snapshot() {
+    SessionSnap& ss = t_snap;
+    const uint64_t v = sessions_version.load(std::memory_order_acquire);
+    if (ss.batcher != id || ss.version != v) {
+        std::lock_guard<std::mutex> lk(smu);
+        ss.s = sessions;
+        ss.batcher = id;
+        ss.version = sessions_version.load(std::memory_order_relaxed);
+    }
+    return ss;
+}
+
+uint64_t cyaes_batcher::enqueued_total() {
+    uint64_t n = 0;
+    for (Shard& sh : shards) {
+        std::lock_guard<std::mutex> lk(sh.mu);
+        n += sh.enqueued;
+    }
+    return n;
+}
+
+// Validates one request and pins its session's schedule.
+int cyaes_batcher::make(const cyaes_batch_req& q, const SessionSnap& ss, Req* r) {
     *r = Req{};
     switch (q.op) {
         case CYAES_OP_ENCRYPT:
@@ -488,9 +607,9 @@ int cyaes_batcher::make(const cyaes_batch_req& q, Req* r) {
         default:
             return CYAES_EINVAL;
     }
-    if (q.slot >= sessions.size() || !sessions[q.slot]) return CYAES_ERANGE;
+    if (q.slot >= ss.s.size() || !ss.s[q.slot]) return CYAES_ERANGE;
     r->op = (uint8_t)q.op;
-    r->key = sessions[q.slot];
+    r->key = ss.s[q.slot];
     r->done = q.done;
     r->user = q.user;
     return CYAES_OK;
@@ -501,17 +620,22 @@ int cyaes_batcher::make(const cyaes_batch_req& q, Req* r) {
 void cyaes_batcher::enqueue(Req* rs, size_t n, uint64_t nbytes) {
     if (n == 0) return;
     const auto t = Clock::now();
-    Shard& sh = shards[my_shard()];
+    const int s = my_shard();
+    Shard& sh = shards[s];
     {
         std::lock_guard<std::mutex> lk(sh.mu);
         for (size_t i = 0; i < n; i++) {
             rs[i].t = t;
             sh.q.push_back(std::move(rs[i]));
         }
+        sh.bytes += nbytes;
+        sh.enqueued += n;
     }
-    submitted.fetch_add(n);
-    int64_t zero = 0;
-    oldest_ns.compare_exchange_strong(zero, now_ns());
+    if (oldest_ns.load(std::memory_order_relaxed) == 0) {  // a plain load while a time is recorded
+        int64_t zero = 0;
+        oldest_ns.compare_exchange_strong(zero, std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                                    t.time_since_epoch()).count());
+    }
     const int64_t before = queued_reqs.fetch_add((int64_t)n);
     const int64_t b0 = queued_bytes.fetch_add((int64_t)nbytes), cap = cfg.max_batch_bytes;
     if (before <= 0 || (b0 < cap && b0 + (int64_t)nbytes >= cap)) {
@@ -582,6 +706,16 @@ void cyaes_batcher_destroy(cyaes_batcher* b) {
     b->cv_submit.notify_all();
     if (b->builder.joinable()) b->builder.join();
     if (b->completer.joinable()) b->completer.join();
+    if (getenv("CYAES_BATCHER_PROFILE") && b->pc.batches) {
+        const Phases &B = b->pb, &C = b->pc;
+        const double nb = (double)C.batches, us = 1e-3;
+        fprintf(stderr,
+                "[cyaes_batcher] %lld batches, %.0f reqs/batch; per batch (us): builder wait %.0f take %.0f form %.0f "
+                "layout %.0f gather %.0f submit %.0f | completer sync %.0f scatter %.0f callbacks %.0f\n",
+                (long long)C.batches, C.reqs / nb, B.wait * us / nb, B.take * us / nb, B.form * us / nb,
+                B.layout * us / nb, B.gather * us / nb, B.submit * us / nb, C.sync * us / nb, C.scatter * us / nb,
+                C.callbacks * us / nb);
+    }
     for (Stage& s : b->stages) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
         if (s.done) (void)hipEventDestroy(s.done);
@@ -604,6 +738,7 @@ int cyaes_batcher_session_open(cyaes_batcher* b, const uint8_t key[16], uint32_t
     while (i < b->sessions.size() && b->sessions[i]) i++;
     if (i == b->sessions.size()) b->sessions.emplace_back();
     b->sessions[i] = std::move(s);
+    b->sessions_version.fetch_add(1, std::memory_order_release);
     *slot = (uint32_t)i;
     return CYAES_OK;
 }
@@ -613,17 +748,14 @@ int cyaes_batcher_session_close(cyaes_batcher* b, uint32_t slot) {
     std::lock_guard<std::mutex> lk(b->smu);
     if (slot >= b->sessions.size() || !b->sessions[slot]) return CYAES_ERANGE;
     b->sessions[slot].reset();
+    b->sessions_version.fetch_add(1, std::memory_order_release);
     return CYAES_OK;
 }
 
 static int submit_one(cyaes_batcher* b, const cyaes_batch_req& q) {
     if (b->stop.load()) return CYAES_EINVAL;
     Req r;
-    int st;
-    {
-        std::lock_guard<std::mutex> lk(b->smu);
-        st = b->make(q, &r);
-    }
+    const int st = b->make(q, b->snapshot(), &r);
     if (st) return st;
     b->enqueue(&r, 1, r.data_bytes());
     return CYAES_OK;
@@ -654,18 +786,16 @@ int cyaes_batcher_submit_many(cyaes_batcher* b, const cyaes_batch_req* reqs, uin
     size_t k = 0;
     uint64_t nbytes = 0;
     int first = CYAES_OK;
-    {
-        std::lock_guard<std::mutex> lk(b->smu);
-        for (uint32_t i = 0; i < n; i++) {
-            const int st = b->make(reqs[i], &rs[k]);
-            if (status) status[i] = st;
-            if (st) {
-                if (first == CYAES_OK) first = st;
-                continue;
-            }
-            nbytes += rs[k].data_bytes();
-            k++;
+    const SessionSnap& ss = b->snapshot();
+    for (uint32_t i = 0; i < n; i++) {
+        const int st = b->make(reqs[i], ss, &rs[k]);
+        if (status) status[i] = st;
+        if (st) {
+            if (first == CYAES_OK) first = st;
+            continue;
         }
+        nbytes += rs[k].data_bytes();
+        k++;
     }
     b->enqueue(rs.data(), k, nbytes);
     return first;
@@ -673,8 +803,8 @@ int cyaes_batcher_submit_many(cyaes_batcher* b, const cyaes_batch_req* reqs, uin
 
 int cyaes_batcher_flush(cyaes_batcher* b) {
     if (!b) return CYAES_EINVAL;
+    const uint64_t target = b->enqueued_total();
     std::unique_lock<std::mutex> lk(b->mu);
-    const uint64_t target = b->submitted.load();
     b->flushers.fetch_add(1);
     b->cv_submit.notify_all();
     b->cv_flush.wait(lk, [&] { return b->completed >= target; });
@@ -686,13 +816,13 @@ int cyaes_batcher_flush(cyaes_batcher* b) {
 
 int cyaes_batcher_stats(cyaes_batcher* b, uint64_t out[6]) {
     if (!b || !out) return CYAES_EINVAL;
-    std::lock_guard<std::mutex> lk(b->mu);
+    std::lock_guard<std::mutex> lk(b->mu);  // completed cannot grow while held: pending >= 0
     out[0] = b->completed;
     out[1] = b->batches;
     out[2] = b->bytes;
     out[3] = b->max_batch;
     out[4] = b->errors;
-    out[5] = b->submitted.load() - b->completed;
+    out[5] = b->enqueued_total() - b->completed;
     return CYAES_OK;
 }
 
