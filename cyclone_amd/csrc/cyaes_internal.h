@@ -37,6 +37,11 @@ constexpr int kEncThreads = 1024;
 constexpr int kEncWgPerCu = 1;
 constexpr int kDecThreads = 1024;
 constexpr int kDecWgPerCu = 1;
+// Encrypt batches with fewer chains than this run four lanes per chain
+// (k_encrypt_quad); larger ones one lane per chain (k_encrypt).
+#ifndef CYAES_QUAD_MAX_CHAINS
+#define CYAES_QUAD_MAX_CHAINS 65536
+#endif
 // Decrypt: blocks per lane per step (a wave step covers 64*kDecRows blocks).
 constexpr int kDecRows = 4;
 
@@ -94,6 +99,8 @@ struct DecArgs {
 
 // Launchers (cyaes_kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t stream);
+// Four lanes per chain (latency-bound batches; threads a multiple of 64).
+hipError_t launch_encrypt_quad(const EncArgs& a, int grid, int threads, hipStream_t stream);
 hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, int threads, hipStream_t stream);
 hipError_t launch_boundary_snapshot(const uint8_t* in, uint64_t nblocks, uint64_t blocks_per_wave,

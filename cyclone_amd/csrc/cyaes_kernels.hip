@@ -475,6 +475,112 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
 
 
 
+// ---- CBC encrypt, latency-bound batches: four lanes per payload chain ------
+// A lane per chain (k_encrypt) fills the chip only with >= 16 waves of chains
+// per CU; below that each wave is a serial chain of ~40 dependent VALU/LDS
+// instructions per round.  Here a quad of lanes shares one chain: lane q owns
+// state word q.  Per round it looks up the four bytes of its own word (T1..T4
+// as tcol) and the quad exchanges them with DPP quad_perm: column j =
+// T1[b0(s_j)] ^ T2[b1(s_j+1)] ^ T3[b2(s_j+2)] ^ T4[b3(s_j+3)] ^ k_j
+// (cyr_rijndael.cpp:659-682), so a round is ~12 instructions on the chain's
+// critical path instead of ~40.  Round-key words are per lane (word q of each
+// round key) in VGPRs, so per-payload keys need no waterfall.
+constexpr uint32_t kQuadFrom1 = 0x39;  // quad_perm [1,2,3,0]: lane j reads lane j+1
+constexpr uint32_t kQuadFrom2 = 0x4E;  // [2,3,0,1]
+constexpr uint32_t kQuadFrom3 = 0x93;  // [3,0,1,2]
+template <uint32_t CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+
+// One AES block on a quad: s = word q of (plaintext ^ chain ^ k0) in, word q of the ciphertext out.
+__device__ __forceinline__ uint32_t enc_block_quad(const char* lds, uint32_t lo, const uint32_t (&k)[11], uint32_t s) {
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        const uint32_t a0 = ld(lds, addr(s, lo, kSel0));                    // T1[b0(s_q)] -> column q
+        const uint32_t a1 = ld(lds, addr1(s, lo));                          // T2[b1(s_q)] -> column q-1
+        const uint32_t a2 = ld(lds + kHalfB, addr(s, lo, kSel2));           // T3[b2(s_q)] -> column q-2
+        const uint32_t a3 = ld(lds + kHalfB, addr(s, lo, region1(kSel3)));  // T4[b3(s_q)] -> column q-3
+        s = xor3(a0, qperm<kQuadFrom1>(a1), xor3(qperm<kQuadFrom2>(a2), qperm<kQuadFrom3>(a3), k[r]));
+    }
+    const uint32_t l0 = ld(lds + kHalfB, addr(s, lo, kSel0));   // S in byte 0 (TL3)
+    const uint32_t l1 = ld(lds + kHalfB, addr1(s, lo));         // byte 1 (TL4)
+    const uint32_t l2 = ld(lds, addr(s, lo, kSel2));            // byte 2 (TL1)
+    const uint32_t l3 = ld(lds, addr(s, lo, region1(kSel3)));   // byte 3 (TL2)
+    return merge4(l0, qperm<kQuadFrom1>(l1), qperm<kQuadFrom2>(l2), qperm<kQuadFrom3>(l3)) ^ k[10];
+}
+
+template <bool RAGGED, bool KEYED>
+__global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_quad(EncArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
+    fill_region(lds_words, a.tables, a.tables + 512, blockDim.x);              // TL1 | TL3
+    fill_region(lds_words + 16384, a.tables + 256, a.tables + 768, blockDim.x);  // TL2 | TL4
+    __shared__ uint32_t lead;  // prio_feedback
+    if (threadIdx.x == 0) lead = 0;
+    uint32_t prog = 0;
+    __syncthreads();
+    const char* lds = reinterpret_cast<const char*>(lds_words);
+    const uint32_t q = threadIdx.x & 3u;
+    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
+    const uint64_t nquads = (uint64_t)gridDim.x * (blockDim.x / 4);
+    // Every lane of a wave runs the loop the same number of times (the bound
+    // is per wave), so a quad never waits in a branch its partners skipped.
+    const uint64_t wq0 = (uint64_t)blockIdx.x * (blockDim.x / 4) + __builtin_amdgcn_readfirstlane(threadIdx.x / 4 & ~15u);
+    for (uint64_t wq = wq0; wq < a.npayloads; wq += nquads) {
+        const uint64_t p = wq + (threadIdx.x / 4 & 15u);
+        if (p >= a.npayloads) continue;
+        uint64_t off;
+        uint32_t nb;
+        if (RAGGED) {
+            off = a.offsets[p];
+            nb = a.nbytes[p] >> 4;
+        } else {
+            off = p * (uint64_t)a.payload_bytes;
+            nb = a.payload_bytes >> 4;
+        }
+        const uint32_t kid = KEYED ? key_index(a.keys, p, true, a.status) : 0u;
+        uint32_t k[11];
+        const uint32_t* sched = a.keys.table + (uint64_t)kid * kSchedWords + q;
+#pragma unroll
+        for (int r = 0; r < 11; r++) k[r] = sched[4 * r];
+        uint32_t c = a.iv_in ? reinterpret_cast<const uint32_t*>(a.iv_in + 16 * p)[q] : (kIv0 + 0x04040404u * q);
+        const uint8_t* src = a.in + off + 4 * q;  // word q of block i at src + 16 i
+        uint8_t* dst = a.out + off + 4 * q;
+        auto ldw = [&](uint32_t i) { return *reinterpret_cast<const uint32_t*>(src + 16ull * i); };
+        uint32_t i = 0;
+        uint32_t b[8];
+        if (nb >= 8) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) b[j] = ldw(j);
+        }
+        for (; i + 8 <= nb; i += 8) {
+            uint32_t bn[8];  // next chunk's loads in flight during this chunk's rounds
+            const bool more = i + 16 <= nb;
+            if (more) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) bn[j] = ldw(i + 8 + j);
+            }
+            prio_feedback(&lead, ++prog, kEncPrioDiv);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                c = enc_block_quad(lds, lo, k, xor3(c, b[j], k[0]));
+                b[j] = c;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) *reinterpret_cast<uint32_t*>(dst + 16ull * (i + j)) = b[j];
+            if (more) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) b[j] = bn[j];
+            }
+        }
+        for (; i < nb; i++) {
+            c = enc_block_quad(lds, lo, k, xor3(c, ldw(i), k[0]));
+            *reinterpret_cast<uint32_t*>(dst + 16ull * i) = c;
+        }
+        if (a.iv_out) reinterpret_cast<uint32_t*>(a.iv_out + 16 * p)[q] = c;
+    }
+}
+
 // ---- CBC decrypt, uniform contiguous batch: one lane per block ------------
 // The batch is one array of nblocks blocks; payload boundaries every bpp
 // blocks restart the chain at the IV.  Each wave owns the contiguous range
@@ -887,6 +993,17 @@ hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t s
     else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false>), g, b, 0, stream, a);
     else if (keyed) hipLaunchKernelGGL((k_encrypt<false, true>), g, b, 0, stream, a);
     else hipLaunchKernelGGL((k_encrypt<false, false>), g, b, 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_encrypt_quad(const EncArgs& a, int grid, int threads, hipStream_t stream) {
+    const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
+    const bool ragged = a.offsets != nullptr;
+    const dim3 g(grid), b(threads);
+    if (ragged && keyed) hipLaunchKernelGGL((k_encrypt_quad<true, true>), g, b, 0, stream, a);
+    else if (ragged) hipLaunchKernelGGL((k_encrypt_quad<true, false>), g, b, 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_encrypt_quad<false, true>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((k_encrypt_quad<false, false>), g, b, 0, stream, a);
     return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ using namespace cyaes;
 struct cyaes_gpu {
     int device = 0;
     int num_cus = 0;
+    uint64_t quad_max_chains = CYAES_QUAD_MAX_CHAINS;  // env CYAES_QUAD_MAX_CHAINS (A/B only)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
     uint32_t* d_keys = nullptr;    // nkeys * kSchedWords
     uint32_t nkeys = 0;
@@ -125,8 +126,14 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.iv_out = iv_out;
     a.tables = ctx->d_tables + kEncTableOff / 4;
     a.status = ctx->d_status;
-    const Shape sh = wave_shape(ctx, (npayloads + 63) / 64, kEncThreads);
     ctx->last_stream = stream;
+    if (npayloads < ctx->quad_max_chains) {
+        // Latency-bound batch (fewer chains than lanes to fill the chip):
+        // four lanes per chain (k_encrypt_quad).
+        const Shape sh = wave_shape(ctx, (4 * npayloads + 63) / 64, kEncThreads);
+        return map_err(launch_encrypt_quad(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
+    }
+    const Shape sh = wave_shape(ctx, (npayloads + 63) / 64, kEncThreads);
     return map_err(launch_encrypt(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
 }
 
@@ -275,6 +282,7 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     cyaes_gpu* ctx = new cyaes_gpu();
     ctx->device = device;
     ctx->num_cus = prop.multiProcessorCount;
+    if (const char* q = getenv("CYAES_QUAD_MAX_CHAINS")) ctx->quad_max_chains = strtoull(q, nullptr, 10);
     const HostTables& t = host_tables();
     uint8_t host[kTablesBytes];
     memcpy(host + kEncTableOff, t.enc, sizeof(t.enc));

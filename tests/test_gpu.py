@@ -25,9 +25,42 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module")
-def ctx(torch):
+# Encrypt has two kernels: four lanes per chain for batches
+# under CYAES_QUAD_MAX_CHAINS chains (every small test batch here), one lane
+# per chain above.  "lane" forces the latter, so both run every test's paths
+# (keys, IVs, ragged, in place); the full-size configs below use it anyway.
+KERNEL_MODES = {"auto": None, "lane": "0"}
+
+
+def _set_mode(mode):
+    old = os.environ.get("CYAES_QUAD_MAX_CHAINS")
+    if KERNEL_MODES[mode] is None:
+        os.environ.pop("CYAES_QUAD_MAX_CHAINS", None)
+    else:
+        os.environ["CYAES_QUAD_MAX_CHAINS"] = KERNEL_MODES[mode]
+    return old
+
+
+def _restore(old):
+    if old is None:
+        os.environ.pop("CYAES_QUAD_MAX_CHAINS", None)
+    else:
+        os.environ["CYAES_QUAD_MAX_CHAINS"] = old
+
+
+@pytest.fixture(params=sorted(KERNEL_MODES))
+def encrypt_kernel(request):
+    """Contexts created inside the test use this encrypt-kernel mode."""
+    old = _set_mode(request.param)
+    yield request.param
+    _restore(old)
+
+
+@pytest.fixture(scope="module", params=sorted(KERNEL_MODES))
+def ctx(torch, request):
+    old = _set_mode(request.param)
     c = ca.GpuContext(0)
+    _restore(old)
     c.set_keys(K0)
     yield c
     c.close()
@@ -102,8 +135,8 @@ def test_dropin_config_sizes(golden):
 
 
 # ------------------------------------------------------------- batch API --
-@pytest.mark.parametrize("pb,n", [(16, 5000), (48, 3001), (64, 1000), (1024, 4096), (1472, 2047), (4096, 257),
-                                  (65280, 65), (65536, 96)])
+@pytest.mark.parametrize("pb,n", [(16, 5000), (48, 3001), (64, 1000), (144, 777), (240, 513), (368, 300),
+                                  (1024, 4096), (1472, 2047), (4096, 257), (65280, 65), (65536, 96)])
 def test_uniform_batch_vs_oracle(torch, ctx, pb, n):
     pt = oracle.synthetic(11, n, pb)
     want = oracle.batch(False, [K0], 0, pt, pb, nthreads=16)
@@ -149,7 +182,7 @@ def test_session_keys_payloads_per_key(torch, ctx):
 
 
 @pytest.mark.parametrize("pb,ppk,nk", [(1472, 256, 6), (65536, 3, 4), (208, 1000, 3)])
-def test_session_keys_uniform_steps(torch, pb, ppk, nk):
+def test_session_keys_uniform_steps(torch, encrypt_kernel, pb, ppk, nk):
     """Sessions spanning many decrypt steps (config D: 256 x 1472 B per key): the
     one-key-per-step fast path, and the steps that straddle a session boundary."""
     n = nk * ppk - 5  # last session partial
@@ -171,7 +204,7 @@ def test_session_keys_uniform_steps(torch, pb, ppk, nk):
 
 # ------------------------------------------------- host-resident batches --
 @pytest.mark.parametrize("pinned", [True, False])
-def test_host_batches_streamed(torch, pinned):
+def test_host_batches_streamed(torch, encrypt_kernel, pinned):
     """cyaes_gpu_{en,de}crypt_host: host memory in and out, several chunks per
     call (3-slot ring wraps), per-session keys, pinned and pageable buffers."""
     nk, ppk, pb = 9, 40, 1472
@@ -217,7 +250,7 @@ def test_host_batch_single_key_large(torch, ctx):
     assert np.array_equal(h_rt, pt)
 
 
-def test_key_index_array_divergent_waves(torch):
+def test_key_index_array_divergent_waves(torch, encrypt_kernel):
     """Arbitrary per-payload key indices: several keys inside one wave (waterfall)."""
     rng = np.random.default_rng(9)
     nk, pb, n = 37, 208, 3000
@@ -267,7 +300,7 @@ def test_iv_in_out(torch, ctx, alias):
     assert np.array_equal(host(d_ivo2).reshape(n, 16), want_iv)  # last ciphertext block
 
 
-def test_ragged_batches(torch):
+def test_ragged_batches(torch, encrypt_kernel):
     """Relay packets of mixed sizes (0..65280 B), gaps between them, per-payload keys and IVs."""
     rng = np.random.default_rng(4)
     n = 700
