@@ -95,6 +95,7 @@ struct DecArgs {
     uint32_t inplace;         // in == out: drain a step's loads before its stores
     const uint32_t* tables;   // kDecTableWords
     uint32_t* status;
+    uint32_t group;           // ragged kernel: payloads per wave group (1..64)
 };
 
 // Launchers (cyaes_kernels.hip).  All asynchronous on `stream`.

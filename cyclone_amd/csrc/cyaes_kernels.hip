@@ -830,7 +830,32 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     }
 }
 
-// ---- CBC decrypt, ragged batch: one wave per payload ----------------------
+// ---- CBC decrypt, ragged batch: groups of payloads packed into wave rows ---
+// A wave takes a group of G consecutive payloads (G <= 64, a.group) and
+// walks their blocks as one flat sequence in steps of R rows x 64 lanes, as
+// k_decrypt_flat does: a row holds the tail of one payload and the head of the
+// next, so 1,472-B relay packets (92 blocks) fill the rows instead of leaving
+// 164 of every 256 lanes idle (one wave per payload).  Lane j of the wave
+// holds payload j's block count, offset and key; a row finds each lane's
+// payload by a binary search over the group's block prefix (ds_bpermute),
+// narrowed to the payloads that start inside the row (usually 0 or 1 step).
+// The predecessor block is the neighbour lane's (DPP), or the IV where a
+// payload starts, so in-place batches need no drain.
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, uint32_t src_lane) {
+    return (uint64_t)bperm((uint32_t)(v >> 32), src_lane) << 32 | bperm((uint32_t)v, src_lane);
+}
+// Lane l's value of v (l wave-uniform).  The builtin returns int: widen as
+// unsigned, or a low word >= 2^31 sign-extends into the high word.
+__device__ __forceinline__ uint64_t rlane64(uint64_t v, uint32_t l) {
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+    return (uint64_t)hi << 32 | lo;
+}
+
+template <bool KEYED>
 __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     constexpr int R = kDecRows;
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
@@ -845,45 +870,123 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
     const uint64_t wave0 =
         (uint64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint64_t p = wave0; p < a.npayloads; p += nwaves) {
-        const uint8_t* in = a.in + a.offsets[p];  // 4-B aligned
-        uint8_t* out = a.out + a.offsets[p];
-        const uint32_t nb = a.nbytes[p] >> 4;
-        uint32_t kid = a.keys.key_idx ? a.keys.key_idx[p] : (a.keys.ppk.d ? fastdiv((uint32_t)p, a.keys.ppk) : 0u);
-        if (kid >= a.keys.nkeys) {
-            if (lane == 0) atomicOr(a.status, 1u);
-            kid = a.keys.nkeys - 1;
+    const uint32_t G = a.group;
+    const uint64_t ngroups = (a.npayloads + G - 1) / G;
+    uint32_t dk0[44];
+    uint32_t dk_id = ~0u;  // session whose schedule dk0 holds
+    if (!KEYED) {
+        load_sched(a.keys.table + 44, dk0);
+        dk_id = 0;
+    }
+    for (uint64_t grp = wave0; grp < ngroups; grp += nwaves) {
+        const uint64_t p0 = grp * G;
+        const uint32_t gn = (uint32_t)min<uint64_t>(G, a.npayloads - p0);
+        const bool holder = lane < gn;
+        const uint64_t ph = p0 + lane;
+        const uint32_t nbh = holder ? a.nbytes[ph] >> 4 : 0u;
+        const uint64_t offh = holder ? a.offsets[ph] : 0ull;
+        const uint32_t kidh = KEYED ? key_index(a.keys, ph, holder, a.status) : 0u;
+        if (holder && nbh == 0 && a.iv_out)  // empty chain: the IV comes back unchanged
+            *reinterpret_cast<uint4*>(a.iv_out + 16 * ph) =
+                a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * ph) : default_iv();
+        // Inclusive prefix of the group's block counts (64-bit: payloads may be up to 2^28 blocks).
+        uint64_t incl = nbh;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t t = (uint64_t)__shfl_up((unsigned int)(incl >> 32), d) << 32 | __shfl_up((unsigned int)incl, d);
+            if (lane >= (uint32_t)d) incl += t;
         }
-        kid = __builtin_amdgcn_readfirstlane(kid);
-        uint32_t dk[44];
-        load_sched(a.keys.table + (uint64_t)kid * kSchedWords + 44, dk);
-        uint4 carry = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
-        if (nb == 0 && a.iv_out && lane == 0) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = carry;  // chain unchanged
-        for (uint32_t base = 0; base < nb; base += 64 * R) {
+        const uint64_t bsh = incl - nbh;  // first flat block of payload `lane`
+        const uint64_t total = rlane64(incl, 63);  // lanes >= gn add 0
+        uint4 carry = make_uint4(0, 0, 0, 0);
+        for (uint64_t base = 0; base < total; base += 64 * R) {
             prio_feedback(leadp, ++prog, kDecPrioDiv);
             uint4 c[R], pv[R];
+            uint32_t jr[R], rr[R];
+            uint64_t orow[R];
+            bool valid[R];
 #pragma unroll
             for (int k = 0; k < R; k++) {
-                const uint32_t g = base + 64 * k + lane;
-                c[k] = g < nb ? ldu(in + 16ull * g) : make_uint4(0, 0, 0, 0);
+                const uint64_t rlo = base + 64 * k;
+                const uint64_t g = rlo + lane;
+                valid[k] = g < total;
+                // Payloads present in the row: jlo (holds rlo) .. jhi (holds the row's last valid block).
+                const uint64_t rhi = min(rlo + 63u, total - 1u);
+                const uint64_t mlo = __ballot(holder && bsh <= rlo);
+                const uint64_t mhi = __ballot(holder && bsh <= rhi);
+                uint32_t j = mlo ? 63u - (uint32_t)__builtin_clzll(mlo) : 0u;
+                const uint32_t jhi = mhi ? 63u - (uint32_t)__builtin_clzll(mhi) : 0u;
+                if (jhi == j) {  // the whole row in one payload (always for large payloads): scalar reads
+                    const uint64_t bs = rlane64(bsh, j);
+                    const uint64_t of = rlane64(offh, j);
+                    rr[k] = (uint32_t)(g - bs);  // < 2^28: within one payload
+                    orow[k] = of + 16ull * rr[k];
+                } else {  // largest j in [jlo, jhi] with bs_j <= g (an empty payload never wins)
+                    uint32_t hi = jhi;
+                    const int steps = 32 - __builtin_clz(jhi - j);
+                    for (int st = 0; st < steps; st++) {
+                        const uint32_t mid = (j + hi + 1) >> 1;
+                        if (bperm64(bsh, mid) <= g) j = mid;
+                        else hi = mid - 1;
+                    }
+                    rr[k] = (uint32_t)(g - bperm64(bsh, j));
+                    orow[k] = bperm64(offh, j) + 16ull * rr[k];
+                }
+                jr[k] = j;
+                c[k] = valid[k] ? ldu(a.in + orow[k]) : make_uint4(0, 0, 0, 0);
             }
-            // predecessors from the neighbour lane (as k_decrypt_flat): no loads of
-            // other lanes' blocks, so in-place needs no drain
             pv[0] = shr1(c[0], carry);
 #pragma unroll
             for (int k = 1; k < R; k++)
                 pv[k] = shr1(c[k], make_uint4(rl63(c[k - 1].x), rl63(c[k - 1].y), rl63(c[k - 1].z), rl63(c[k - 1].w)));
 #pragma unroll
             for (int k = 0; k < R; k++) {
-                const uint32_t g = base + 64 * k + lane;
-                if (a.iv_out && g + 1 == nb) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+                const uint64_t p = p0 + jr[k];
+                if (valid[k] && rr[k] == 0)
+                    pv[k] = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
+                const uint32_t nbj = bperm(nbh, jr[k]);  // all lanes: a bpermute from an inactive lane reads 0
+                if (a.iv_out && valid[k] && rr[k] + 1 == nbj) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
             }
-            dec_cbc<R>(lds, lo, dk, c, pv);
+            if (!KEYED) {
+                dec_cbc<R>(lds, lo, dk0, c, pv);
+            } else {
+                uint32_t kid[R];
 #pragma unroll
-            for (int k = 0; k < R; k++) {
-                const uint32_t g = base + 64 * k + lane;
-                if (g < nb) stu(out + 16ull * g, pv[k]);
+                for (int k = 0; k < R; k++) kid[k] = bperm(kidh, jr[k]);
+                const uint32_t k0 = __builtin_amdgcn_readfirstlane(kid[0]);  // lane 0 of row 0 is valid
+                bool same = true;
+#pragma unroll
+                for (int k = 0; k < R; k++) same = same && (!valid[k] || kid[k] == k0);
+                if (__ballot(!same) == 0) {  // one session in the whole step (the common case)
+                    if (k0 != dk_id) {
+                        load_sched(a.keys.table + (uint64_t)k0 * kSchedWords + 44, dk0);
+                        dk_id = k0;
+                    }
+                    dec_cbc<R>(lds, lo, dk0, c, pv);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < R; k++) {
+                        bool pending = valid[k];
+                        while (true) {  // waterfall over the sessions of this row
+                            const uint64_t m = __ballot(pending);
+                            if (m == 0) break;
+                            const uint32_t ku = __builtin_amdgcn_readlane(kid[k], __builtin_ctzll(m));
+                            if (pending && kid[k] == ku) {
+                                pending = false;
+                                uint32_t dk[44];
+                                load_sched(a.keys.table + (uint64_t)ku * kSchedWords + 44, dk);
+                                const uint4 cc[1] = {c[k]};
+                                uint4 dd[1] = {pv[k]};
+                                dec_cbc<1>(lds, lo, dk, cc, dd);
+                                pv[k] = dd[0];
+                            }
+                        }
+                    }
+                }
             }
+#pragma unroll
+            for (int k = 0; k < R; k++)
+                if (valid[k]) stu(a.out + orow[k], pv[k]);
             carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
         }
     }
@@ -1019,7 +1122,9 @@ hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream) {
 }
 
 hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, int threads, hipStream_t stream) {
-    hipLaunchKernelGGL(k_decrypt_ragged, dim3(grid), dim3(threads), 0, stream, a);
+    const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
+    if (keyed) hipLaunchKernelGGL(k_decrypt_ragged<true>, dim3(grid), dim3(threads), 0, stream, a);
+    else hipLaunchKernelGGL(k_decrypt_ragged<false>, dim3(grid), dim3(threads), 0, stream, a);
     return hipGetLastError();
 }
 

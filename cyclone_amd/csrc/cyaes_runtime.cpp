@@ -18,6 +18,7 @@ struct cyaes_gpu {
     int device = 0;
     int num_cus = 0;
     uint64_t quad_max_chains = CYAES_QUAD_MAX_CHAINS;  // env CYAES_QUAD_MAX_CHAINS (A/B only)
+    uint32_t ragged_group = 0;  // env CYAES_RAGGED_GROUP: payloads per ragged-decrypt wave group (0 = auto; tests, A/B)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
     uint32_t* d_keys = nullptr;    // nkeys * kSchedWords
     uint32_t nkeys = 0;
@@ -207,7 +208,14 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.tables = ctx->d_tables + kDecTableOff / 4;
     a.status = ctx->d_status;
     a.inplace = in == out;
-    const Shape sh = wave_shape(ctx, npayloads, kDecThreads);
+    // Payloads per wave group: as many as keep >= 2 groups per wave of a full
+    // grid (balance), up to 64 (one holder lane each); small payloads then
+    // share rows.  Sweep in profiles/r01/ab_ragged_groups.txt.
+    const uint64_t slots = (uint64_t)std::max(1, ctx->num_cus) * (kDecThreads / 64);
+    const uint64_t G = ctx->ragged_group ? ctx->ragged_group
+                                         : std::min<uint64_t>(64, std::max<uint64_t>(1, npayloads / (2 * slots)));
+    a.group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, G));
+    const Shape sh = wave_shape(ctx, (npayloads + a.group - 1) / a.group, kDecThreads);
     ctx->last_stream = stream;
     return map_err(launch_decrypt_ragged(a, std::min(sh.grid, dec_grid_cap(ctx)), sh.threads, stream));
 }
@@ -283,6 +291,7 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     ctx->device = device;
     ctx->num_cus = prop.multiProcessorCount;
     if (const char* q = getenv("CYAES_QUAD_MAX_CHAINS")) ctx->quad_max_chains = strtoull(q, nullptr, 10);
+    if (const char* g = getenv("CYAES_RAGGED_GROUP")) ctx->ragged_group = (uint32_t)strtoul(g, nullptr, 10);
     const HostTables& t = host_tables();
     uint8_t host[kTablesBytes];
     memcpy(host + kEncTableOff, t.enc, sizeof(t.enc));

@@ -346,6 +346,111 @@ def test_ragged_batches(torch, encrypt_kernel):
     c.close()
 
 
+@pytest.fixture(params=["1", "3", "64", "auto"])
+def ragged_group(request):
+    """Payloads per wave group of the ragged decrypt: forced, or the runtime's choice."""
+    old = os.environ.get("CYAES_RAGGED_GROUP")
+    if request.param == "auto":
+        os.environ.pop("CYAES_RAGGED_GROUP", None)
+    else:
+        os.environ["CYAES_RAGGED_GROUP"] = request.param
+    yield request.param
+    if old is None:
+        os.environ.pop("CYAES_RAGGED_GROUP", None)
+    else:
+        os.environ["CYAES_RAGGED_GROUP"] = old
+
+
+@pytest.mark.parametrize("keying", ["one", "index", "ppk"])
+def test_ragged_decrypt_groups(torch, ragged_group, keying):
+    """Relay-packet streams in HBM (payload at packet offset 12, 4-B aligned):
+    mostly small packets with empty and one-block ones, a few 65,280-B ones;
+    rows of a wave span several payloads (group > 1).  Keys per payload
+    (index array, sessions of 7 payloads) or one key; IV in/out; in place."""
+    rng = np.random.default_rng(21)
+    n = 2500
+    blocks = rng.choice([0, 1, 2, 5, 63, 64, 65, 92, 200], n).astype(np.uint32)
+    blocks[rng.integers(0, n, 12)] = 4080
+    sizes = blocks * 16
+    offsets = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for p in range(n):
+        offsets[p] = pos + 12  # packet header: 4-B head + 8-B forward msg
+        pos += 12 + int(sizes[p])
+    nk = 9
+    keys = [bytes(rng.integers(0, 256, 16, dtype=np.uint8)) for _ in range(nk)]
+    ppk = 7 if keying == "ppk" else 0
+    if keying == "index":
+        kidx = rng.integers(0, nk, n, dtype=np.uint32)
+    elif keying == "ppk":
+        kidx = (np.arange(n) // ppk % nk).astype(np.uint32)
+        keys = [keys[(s) % nk] for s in range(n // ppk + 1)]
+    else:
+        kidx = np.zeros(n, dtype=np.uint32)
+    ivs = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    plain = rng.integers(0, 256, pos, dtype=np.uint8)
+    ct = plain.copy()
+    for p in range(n):
+        o, s = int(offsets[p]), int(sizes[p])
+        k = keys[p // ppk] if ppk else keys[kidx[p]]
+        ct[o:o + s] = np.frombuffer(bytes(oracle.Rijndael(k).encrypt(plain[o:o + s].tobytes(), None, s,
+                                                                      bytearray(ivs[p].tobytes()))), np.uint8)
+    c = ca.GpuContext(0)
+    c.set_keys(b"".join(keys))
+    d_off, d_nb = dev(torch, offsets), dev(torch, sizes)
+    d_k = dev(torch, kidx) if keying == "index" else None
+    d_iv, d_ivo = dev(torch, ivs), empty(torch, ivs.size)
+    d_ct, d_back = dev(torch, ct), dev(torch, ct)  # headers / untouched bytes keep their values
+    c.decrypt_ragged(d_ct, d_back, d_off, d_nb, n, key_idx=d_k, payloads_per_key=ppk, iv_in=d_iv, iv_out=d_ivo)
+    got = host(d_back)
+    for p in np.flatnonzero(sizes):
+        o, s = int(offsets[p]), int(sizes[p])
+        assert np.array_equal(got[o:o + s], plain[o:o + s]), (p, int(blocks[p]))
+    hdr = np.ones(pos, dtype=bool)
+    for p in range(n):
+        hdr[int(offsets[p]):int(offsets[p]) + int(sizes[p])] = False
+    assert np.array_equal(got[hdr], ct[hdr])  # nothing outside the payloads is written
+    got_iv = host(d_ivo).reshape(n, 16)
+    for p in range(n):
+        o, s = int(offsets[p]), int(sizes[p])
+        assert np.array_equal(got_iv[p], ct[o + s - 16:o + s] if s else ivs[p]), p
+    c.decrypt_ragged(d_ct, d_ct, d_off, d_nb, n, key_idx=d_k, payloads_per_key=ppk, iv_in=d_iv)  # in place
+    assert np.array_equal(host(d_ct), got)
+    assert c.check() == ca.CYAES_OK
+    c.close()
+
+
+def test_ragged_offsets_beyond_4gib(torch, ragged_group, encrypt_kernel):
+    """Payload offsets >= 2^31 and >= 2^32 (a batch base pointer far below the
+    data): the 64-bit offset arithmetic of both ragged kernels."""
+    rng = np.random.default_rng(5)
+    n = 300
+    sizes = (rng.choice([0, 1, 3, 92, 300], n) * 16).astype(np.uint32)
+    offsets = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for p in range(n):
+        offsets[p] = pos
+        pos += int(sizes[p]) + 12
+    data = rng.integers(0, 256, pos, dtype=np.uint8)
+    want = data.copy()
+    for p in range(n):
+        o, s = int(offsets[p]), int(sizes[p])
+        want[o:o + s] = np.frombuffer(bytes(oracle.Rijndael(K0).encrypt(data[o:o + s].tobytes())), np.uint8)
+    c = ca.GpuContext(0)
+    c.set_keys(K0)
+    for bias in ((1 << 31) + 4, (5 << 32) + 1024):
+        d = dev(torch, data)
+        base = d.data_ptr() - bias  # in/out point `bias` bytes below the data
+        d_off = dev(torch, offsets + np.uint64(bias))
+        d_nb = dev(torch, sizes)
+        c.encrypt_ragged(base, base, d_off, d_nb, n)
+        assert np.array_equal(host(d), want)
+        c.decrypt_ragged(base, base, d_off, d_nb, n)
+        assert np.array_equal(host(d), data)
+    assert c.check() == ca.CYAES_OK
+    c.close()
+
+
 def test_device_key_expansion(torch):
     """Keys already on the device (e.g. after the RCCL broadcast) are expanded there."""
     rng = np.random.default_rng(12)
