@@ -37,11 +37,15 @@ constexpr int kEncThreads = 1024;
 constexpr int kEncWgPerCu = 1;
 constexpr int kDecThreads = 1024;
 constexpr int kDecWgPerCu = 1;
-// Encrypt batches with fewer chains than this run four lanes per chain
-// (k_encrypt_quad); larger ones one lane per chain (k_encrypt).
+// Uniform encrypt batches with fewer chains than this run four lanes per
+// chain (k_encrypt_quad), larger ones one lane per chain (k_encrypt); ragged
+// batches switch at kQuadRaggedFactor times the count, because relay packets
+// (payload at packet offset 12) are not 16-B aligned and the quad kernel's
+// dword accesses lose less to that (tools/ab_quad.py, tools/ab_ragged.py).
 #ifndef CYAES_QUAD_MAX_CHAINS
-#define CYAES_QUAD_MAX_CHAINS 65536
+#define CYAES_QUAD_MAX_CHAINS 131072
 #endif
+constexpr uint64_t kQuadRaggedFactor = 16;
 // Decrypt: blocks per lane per step (a wave step covers 64*kDecRows blocks).
 constexpr int kDecRows = 4;
 

@@ -128,9 +128,11 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.tables = ctx->d_tables + kEncTableOff / 4;
     a.status = ctx->d_status;
     ctx->last_stream = stream;
-    if (npayloads < ctx->quad_max_chains) {
-        // Latency-bound batch (fewer chains than lanes to fill the chip):
-        // four lanes per chain (k_encrypt_quad).
+    const uint64_t q = ctx->quad_max_chains;
+    const uint64_t quad_max = !offsets ? q : (q > UINT64_MAX / kQuadRaggedFactor ? UINT64_MAX : q * kQuadRaggedFactor);
+    if (npayloads < quad_max) {
+        // Latency-bound batch (fewer chains than lanes to fill the chip four
+        // times over), or a ragged one: four lanes per chain (k_encrypt_quad).
         const Shape sh = wave_shape(ctx, (4 * npayloads + 63) / 64, kEncThreads);
         return map_err(launch_encrypt_quad(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
     }
