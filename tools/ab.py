@@ -3,6 +3,7 @@
 (MI355X_MICROARCH.md: never rank builds by timings from different runs/devices).
 
 usage: python tools/ab.py build/variants/a.so build/variants/b.so [--rounds 6] [--payloads N]
+       [--payload-bytes B] [--ppk K]   (--ppk: sessions of K payloads, config D's keys)
 Each round runs every variant's encrypt and decrypt once on the same config-C
 buffers; prints per-variant median/min ms per kernel and checks the outputs agree.
 """
@@ -21,6 +22,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--payloads", type=int, default=262144)
     ap.add_argument("--payload-bytes", type=int, default=65536)
+    ap.add_argument("--ppk", type=int, default=0, help="payloads per session key (0: one key)")
     args = ap.parse_args()
     import torch
     import cyclone_amd as ca
@@ -31,7 +33,11 @@ def main():
     for path in args.libs:
         lib = ca.load_library(os.path.abspath(path))
         c = ca.GpuContext(0, lib=lib)
-        c.set_keys(bytes(range(16)))
+        if args.ppk:
+            import bench
+            c.set_keys(bench.session_keys((args.payloads + args.ppk - 1) // args.ppk))
+        else:
+            c.set_keys(bytes(range(16)))
         ctxs.append(c)
     pt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     ct = torch.empty_like(pt)
@@ -45,9 +51,9 @@ def main():
         for path, c in zip(args.libs, ctxs):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record(s)
-            c.encrypt_uniform(pt, ct, n, pb, stream=s.cuda_stream)
+            c.encrypt_uniform(pt, ct, n, pb, payloads_per_key=args.ppk, stream=s.cuda_stream)
             e[1].record(s)
-            c.decrypt_uniform(ct, rt, n, pb, stream=s.cuda_stream)
+            c.decrypt_uniform(ct, rt, n, pb, payloads_per_key=args.ppk, stream=s.cuda_stream)
             e[2].record(s)
             torch.cuda.synchronize()
             if r == 0:  # warm-up round; check outputs
