@@ -411,7 +411,10 @@ int cyaes_batcher::launch(Stage* st) {
     // a wave (cyaes_kernels.hip, k_encrypt), so order its list by key: a wave
     // then sees one key, two at a boundary, instead of one per looper thread.
     // (Decrypt runs one payload per wave: one key per wave already.)
-    if (klist.size() > 1 && !eo.empty()) {
+    // (Only for the lane-per-chain kernel: below its threshold the ragged
+    // encrypt runs four lanes per chain with per-chain keys, and order does
+    // not matter.)
+    if (klist.size() > 1 && !eo.empty() && !cyaes::ragged_encrypt_is_quad(ctx, eo.size())) {
         // Stable counting sort by key index (key indices are dense: 0..klist.size()-1).
         std::vector<uint64_t>& o2 = lists.o2;
         std::vector<uint32_t>&l2 = lists.l2, &k2 = lists.k2, &at = lists.at;

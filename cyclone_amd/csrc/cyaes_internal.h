@@ -119,6 +119,9 @@ hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long
 // Host runtime (cyaes_runtime.cpp): ragged batch under an explicit device key
 // table of table_keys schedules (the batcher's per-batch session keys).
 // key_idx (device, nullable => key 0) indexes that table.
+// True when a ragged encrypt of n chains runs four lanes per chain
+// (k_encrypt_quad: per-chain keys, no key waterfall, so no need to sort by key).
+bool ragged_encrypt_is_quad(const cyaes_gpu* ctx, uint64_t n);
 int ragged_batch(cyaes_gpu* ctx, bool decrypt, const uint32_t* d_table, uint32_t table_keys, const uint8_t* in,
                  uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes, uint64_t npayloads,
                  const uint32_t* key_idx, hipStream_t stream);

@@ -110,6 +110,15 @@ Shape wave_shape(const cyaes_gpu* ctx, uint64_t waves, int max_threads) {
     return {(int)std::max<uint64_t>(1, (waves + w - 1) / w), (int)(64 * w)};
 }
 
+}  // namespace
+
+bool cyaes::ragged_encrypt_is_quad(const cyaes_gpu* ctx, uint64_t n) {
+    const uint64_t q = ctx->quad_max_chains;
+    return n < (q > UINT64_MAX / kQuadRaggedFactor ? UINT64_MAX : q * kQuadRaggedFactor);
+}
+
+namespace {
+
 int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
                    uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk,
                    const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream, const uint32_t* table = nullptr,
@@ -128,9 +137,7 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.tables = ctx->d_tables + kEncTableOff / 4;
     a.status = ctx->d_status;
     ctx->last_stream = stream;
-    const uint64_t q = ctx->quad_max_chains;
-    const uint64_t quad_max = !offsets ? q : (q > UINT64_MAX / kQuadRaggedFactor ? UINT64_MAX : q * kQuadRaggedFactor);
-    if (npayloads < quad_max) {
+    if (offsets ? ragged_encrypt_is_quad(ctx, npayloads) : npayloads < ctx->quad_max_chains) {
         // Latency-bound batch (fewer chains than lanes to fill the chip four
         // times over), or a ragged one: four lanes per chain (k_encrypt_quad).
         const Shape sh = wave_shape(ctx, (4 * npayloads + 63) / 64, kEncThreads);
