@@ -100,6 +100,7 @@ struct DecArgs {
     const uint32_t* tables;   // kDecTableWords
     uint32_t* status;
     uint32_t group;           // ragged kernel: payloads per wave group (1..64)
+    uint64_t sess_blocks;     // flat kernel: blocks per payloads_per_key session when a multiple of a step, else 0
 };
 
 // Launchers (cyaes_kernels.hip).  All asynchronous on `stream`.

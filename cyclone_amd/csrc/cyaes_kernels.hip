@@ -773,7 +773,11 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
     return make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));  // next carry
 }
 
-template <bool KEYED, bool BIG>
+// SESS: sessions of payloads_per_key payloads that are whole steps long
+// (a.sess_blocks, a multiple of 64 * R; config D: 256 x 92 blocks): no step
+// straddles two sessions, so the unkeyed step runs under a schedule chosen per
+// step from the scalar block position, and no lane computes a key index.
+template <bool KEYED, bool BIG, bool SESS>
 __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     constexpr int R = kDecRows;
     static_assert(R % 2 == 0, "rows are decrypted in pairs");
@@ -799,12 +803,26 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     if (ps.bpos != 0) carry = a.boundary ? a.boundary[wave] : reinterpret_cast<const uint4*>(a.in)[begin - 1];
     uint32_t dk0[44];
     uint32_t dk_id = 0;  // KEYED: session whose schedule dk0 holds (~0u: none yet)
-    if (!KEYED) load_sched(a.keys.table + 44, dk0);
-    else dk_id = ~0u;
+    uint32_t sess = 0;   // SESS: session of the current step; it ends at block sess_next
+    uint64_t sess_next = 0;
+    if (SESS) {
+        sess = (uint32_t)(begin / a.sess_blocks);
+        sess_next = (uint64_t)(sess + 1) * a.sess_blocks;
+        load_sched(a.keys.table + (uint64_t)sess * kSchedWords + 44, dk0);
+    } else if (!KEYED) {
+        load_sched(a.keys.table + 44, dk0);
+    } else {
+        dk_id = ~0u;
+    }
     uint64_t base = begin;
     uint4 c[R], pv[R];
     if (base + 64 * R <= end) flat_load<true>(a, lane, base, end, c, pv);
     for (; base + 64 * R <= end; base += 64 * R) {
+        if (SESS && base >= sess_next) {  // (make_keysel checked every session is in the table)
+            sess++;
+            sess_next += a.sess_blocks;
+            load_sched(a.keys.table + (uint64_t)sess * kSchedWords + 44, dk0);
+        }
 #if !CYAES_DEC_PREFETCH  // A/B (tools/ab.py): prefetching the next step costs ~1% here
         carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv);
         if (base + 128 * R <= end) flat_load<true>(a, lane, base + 64 * R, end, c, pv);
@@ -825,6 +843,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
         if (ps.bpos >= a.bpp.d) { ps.bpos -= a.bpp.d; ps.bp++; }
     }
     if (base < end) {
+        if (SESS && base >= sess_next) load_sched(a.keys.table + (uint64_t)(sess + 1) * kSchedWords + 44, dk0);
         flat_load<false>(a, lane, base, end, c, pv);
         flat_step<KEYED, BIG, false>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv);
     }
@@ -1114,10 +1133,13 @@ hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
     const bool big = a.bpp.d >= 64u * kDecRows;
     const dim3 g(grid), b(kDecThreads);
-    if (keyed && big) hipLaunchKernelGGL((k_decrypt_flat<true, true>), g, b, 0, stream, a);
-    else if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true, false>), g, b, 0, stream, a);
-    else if (big) hipLaunchKernelGGL((k_decrypt_flat<false, true>), g, b, 0, stream, a);
-    else hipLaunchKernelGGL((k_decrypt_flat<false, false>), g, b, 0, stream, a);
+    const bool sess = a.sess_blocks != 0;  // keyed by step-aligned sessions: the unkeyed step per session
+    if (sess && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, true>), g, b, 0, stream, a);
+    else if (sess) hipLaunchKernelGGL((k_decrypt_flat<false, false, true>), g, b, 0, stream, a);
+    else if (keyed && big) hipLaunchKernelGGL((k_decrypt_flat<true, true, false>), g, b, 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true, false, false>), g, b, 0, stream, a);
+    else if (big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((k_decrypt_flat<false, false, false>), g, b, 0, stream, a);
     return hipGetLastError();
 }
 

@@ -189,6 +189,10 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     a.tables = ctx->d_tables + kDecTableOff / 4;
     a.status = ctx->d_status;
     a.inplace = in == out;
+    // Sessions of payloads_per_key payloads that are whole steps long: every
+    // step lies in one session (the kernel picks its schedule per step).
+    const uint64_t sess_blocks = (uint64_t)ppk * bpp;
+    if (!key_idx && ppk && sess_blocks % step == 0) a.sess_blocks = sess_blocks;
     if (in == out && nwaves > 1) {
         st = ensure(&ctx->d_boundary, &ctx->boundary_cap, nwaves);
         if (st) return st;

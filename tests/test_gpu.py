@@ -181,10 +181,13 @@ def test_session_keys_payloads_per_key(torch, ctx):
     c.close()
 
 
-@pytest.mark.parametrize("pb,ppk,nk", [(1472, 256, 6), (65536, 3, 4), (208, 1000, 3)])
+@pytest.mark.parametrize("pb,ppk,nk", [(1472, 256, 6), (65536, 3, 4), (208, 1000, 3), (4096, 1, 700), (1024, 16, 300)])
 def test_session_keys_uniform_steps(torch, encrypt_kernel, pb, ppk, nk):
-    """Sessions spanning many decrypt steps (config D: 256 x 1472 B per key): the
-    one-key-per-step fast path, and the steps that straddle a session boundary."""
+    """Sessions spanning many decrypt steps (config D: 256 x 1472 B per key).
+    Sessions that are whole steps long (1472 x 256, 65536 x 3, 4096 x 1, 1024 x 16)
+    take the session-aligned decrypt (schedule chosen per step, several sessions
+    per wave); 208 x 1000 takes the per-lane one-key-per-step check and the
+    waterfall of steps that straddle a session boundary."""
     n = nk * ppk - 5  # last session partial
     keys = [oracle.session_key(100 + s) for s in range(nk)]
     c = ca.GpuContext(0)
