@@ -24,11 +24,15 @@
 //    a per-payload key index is handled by a waterfall over the distinct keys
 //    present in a wave, normally one).
 //  * Encrypt (serial CBC): one lane = one payload chain, 8 blocks (128 B, one
-//    full line per lane) loaded per step.
+//    full line per lane) loaded per step (k_encrypt).  Batches with too few
+//    chains to fill the chip, and ragged ones, use four lanes per chain, one
+//    state word each, exchanging lookups by DPP quad_perm (k_encrypt_quad).
 //  * Decrypt (block-parallel): one lane = one 16-B block, four rows decrypted
 //    together, each wave-instruction loads 1 KiB contiguous; the previous
 //    ciphertext block comes from the neighbour lane (DPP wave_shr:1), the
-//    wave's chain across rows and steps through readlane 63.
+//    wave's chain across rows and steps through readlane 63 (k_decrypt_flat;
+//    sessions that are whole steps pick their schedule per step).  Ragged
+//    batches pack groups of up to 64 payloads into the rows (k_decrypt_ragged).
 //  * Waves of a workgroup are kept level by progress-feedback priority
 //    (prio_feedback), so none runs a starved tail.
 #include "cyaes_internal.h"
