@@ -1,0 +1,146 @@
+"""Randomized parity sweep over the batch API (GPU): every kernel choice the
+runtime can make for encrypt and decrypt, against the oracle, bit-exact.
+
+Each case draws a batch shape, key mode, IV mode and layout from a seeded
+generator and forces the kernel choice through the runtime's A/B knobs:
+  encrypt  CYAES_QUAD_MAX_CHAINS   lane per chain / four lanes per chain
+  decrypt  CYAES_RAGGED_GROUP      payloads per wave group of the ragged kernel
+Layouts: uniform (flat decrypt, incl. the session-aligned keyed path) and
+ragged relay-packet streams (payload at packet offset 12, gaps, empties).
+Semantics: Rijndael::encrypt/decrypt per payload (cyr_rijndael.cpp:588-635),
+IV in/out per payload, in place allowed."""
+import os
+
+import numpy as np
+import pytest
+
+import cyclone_amd as ca
+import oracle
+
+pytestmark = pytest.mark.gpu
+NCASES = 160
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "gpu tests need a ROCm device"
+    return t
+
+
+def dev(torch, arr):
+    a = np.ascontiguousarray(arr)
+    return torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to("cuda")
+
+
+def host(t):
+    import torch as _t
+    _t.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def context(env):
+    old = {k: os.environ.get(k) for k in env}
+    try:
+        for k, v in env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        return ca.GpuContext(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def draw_case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    layout = rng.choice(["uniform", "ragged"])
+    n = int(rng.choice([1, 7, 63, 64, 65, 300, 1000, 2500]))
+    if layout == "uniform":
+        blocks = np.full(n, int(rng.choice([1, 3, 8, 9, 15, 16, 23, 92, 256, 300])), dtype=np.uint32)
+    else:
+        blocks = rng.choice([0, 1, 2, 5, 7, 8, 9, 16, 63, 64, 65, 92, 257], n).astype(np.uint32)
+        blocks[rng.integers(0, n, max(1, n // 200))] = int(rng.choice([600, 4080]))
+    keying = rng.choice(["one", "index", "ppk"])
+    ppk = int(rng.choice([1, 2, 7, 16, 64])) if keying == "ppk" else 0
+    return dict(
+        rng=rng, layout=layout, n=n, blocks=blocks, keying=keying, ppk=ppk,
+        iv_in=bool(rng.integers(0, 2)), iv_out=bool(rng.integers(0, 2)), inplace=bool(rng.integers(0, 2)),
+        env={"CYAES_QUAD_MAX_CHAINS": str(rng.choice(["0", str(1 << 40)])) if rng.integers(0, 3) else None,
+             "CYAES_RAGGED_GROUP": str(rng.choice([1, 2, 5, 64])) if rng.integers(0, 3) else None})
+
+
+@pytest.mark.parametrize("seed", range(NCASES))
+def test_batch_sweep(torch, seed):
+    k = draw_case(seed)
+    rng, n, blocks, ppk = k["rng"], k["n"], k["blocks"], k["ppk"]
+    sizes = blocks * 16
+    nk = (n - 1) // ppk + 1 if ppk else 11
+    keys = [bytes(rng.integers(0, 256, 16, dtype=np.uint8)) for _ in range(nk)]
+    kidx = rng.integers(0, nk, n, dtype=np.uint32) if k["keying"] == "index" else None
+
+    def key_of(p):
+        if k["keying"] == "index":
+            return keys[kidx[p]]
+        return keys[p // ppk] if ppk else keys[0]
+
+    if k["layout"] == "uniform":
+        offsets = np.arange(n, dtype=np.uint64) * int(sizes[0])
+        total = int(n * int(sizes[0]))
+    else:
+        offsets = np.zeros(n, dtype=np.uint64)
+        pos = 0
+        gaps = rng.integers(0, 3, n) * 4
+        for p in range(n):
+            pos += 12 + int(gaps[p])
+            offsets[p] = pos
+            pos += int(sizes[p])
+        total = pos
+    ivs = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    plain = rng.integers(0, 256, max(total, 16), dtype=np.uint8)
+    ct, want_iv = plain.copy(), np.empty_like(ivs)
+    for p in range(n):
+        o, s = int(offsets[p]), int(sizes[p])
+        iv = bytearray(ivs[p].tobytes() if k["iv_in"] else oracle.default_iv())
+        ct[o:o + s] = np.frombuffer(bytes(oracle.Rijndael(key_of(p)).encrypt(plain[o:o + s].tobytes(), None, s, iv)),
+                                    np.uint8)
+        want_iv[p] = np.frombuffer(bytes(iv), np.uint8)  # final chain (unchanged for an empty payload)
+
+    c = context(k["env"])
+    try:
+        c.set_keys(b"".join(keys))
+        kw = dict(key_idx=dev(torch, kidx) if kidx is not None else None, payloads_per_key=ppk)
+        d_ivi = dev(torch, ivs) if k["iv_in"] else None
+        d_ivo = torch.zeros(n * 16, dtype=torch.uint8, device="cuda") if k["iv_out"] else None
+        d_pt = dev(torch, plain)
+        d_ct = d_pt if k["inplace"] else dev(torch, plain)  # out starts as a copy: gaps keep their bytes
+        if k["layout"] == "uniform":
+            c.encrypt_uniform(d_pt, d_ct, n, int(sizes[0]), iv_in=d_ivi, iv_out=d_ivo, **kw)
+        else:
+            d_off, d_nb = dev(torch, offsets), dev(torch, sizes)
+            c.encrypt_ragged(d_pt, d_ct, d_off, d_nb, n, iv_in=d_ivi, iv_out=d_ivo, **kw)
+        got = host(d_ct)
+        assert np.array_equal(got[:total], ct[:total]), k
+        if k["iv_out"]:
+            assert np.array_equal(host(d_ivo).reshape(n, 16), want_iv), k
+        # decrypt the ciphertext back; the IV out of a decrypt is the last ciphertext block
+        d_src = dev(torch, ct)
+        d_back = d_src if k["inplace"] else dev(torch, ct)
+        d_ivo2 = torch.zeros(n * 16, dtype=torch.uint8, device="cuda") if k["iv_out"] else None
+        if k["layout"] == "uniform":
+            c.decrypt_uniform(d_src, d_back, n, int(sizes[0]), iv_in=d_ivi, iv_out=d_ivo2, **kw)
+        else:
+            c.decrypt_ragged(d_src, d_back, d_off, d_nb, n, iv_in=d_ivi, iv_out=d_ivo2, **kw)
+        assert np.array_equal(host(d_back)[:total], plain[:total]), k
+        if k["iv_out"]:
+            exp = np.array([ct[int(offsets[p]) + int(sizes[p]) - 16:int(offsets[p]) + int(sizes[p])]
+                            if sizes[p] else (ivs[p] if k["iv_in"] else np.frombuffer(oracle.default_iv(), np.uint8))
+                            for p in range(n)])
+            assert np.array_equal(host(d_ivo2).reshape(n, 16), exp), k
+        assert c.check() == ca.CYAES_OK
+    finally:
+        c.close()
