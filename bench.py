@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--packet-configs", default="B,D",
                     help="other BASELINE.json packet configs measured after the headline one ('none' to skip)")
     ap.add_argument("--packet-steps", type=int, default=20)
+    ap.add_argument("--packet-warmup", type=int, default=20,
+                    help="untimed steps before each packet config (a 1,472-B step is ~2 ms; 20 cover the clock "
+                         "ramp that 2 steps of the 23-ms headline step cover, profiles/r01/packet_warmup.txt)")
     return ap.parse_args()
 
 
@@ -280,10 +283,10 @@ def main():
     for name in ([] if args.packet_configs == "none" else args.packet_configs.split(",")):
         if name == args.config or name not in CONFIGS:
             continue
-        r = run_config(name, CONFIGS[name][0], args.packet_steps, 2, not args.no_verify)
+        r = run_config(name, CONFIGS[name][0], args.packet_steps, args.packet_warmup, not args.no_verify)
         packet_configs[name] = {
             "value": round(r["value"], 2), "unit": "GiB/s", "ms_per_step": round(r["t"] / r["steps"] * 1e3, 4),
-            "steps": r["steps"], "payloads_per_gpu": r["npay"], "payload_bytes": r["pb"],
+            "steps": r["steps"], "warmup": args.packet_warmup, "payloads_per_gpu": r["npay"], "payload_bytes": r["pb"],
             "payloads_per_key": r["ppk"], "encrypt_ms": round(r["enc_ms"], 4), "decrypt_ms": round(r["dec_ms"], 4),
             "hbm_frac_step": round(4.0 * r["nbytes"] / (r["t"] / r["steps"]) / 1e9 / HBM_PEAK_GBS, 4),
             "parity": r["parity"],
