@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <mutex>
 #include <vector>
 
@@ -538,16 +539,41 @@ int cyaes_gpu_digest(const uint8_t* d_buf, uint64_t nbytes, uint64_t out[2], voi
 }  // extern "C"
 
 // ---- host-memory drop-in (Rijndael::encrypt / decrypt) --------------------
+// Every call is one CBC chain (cyr_rijndael.cpp:588-635), synchronous, and a
+// lone chain on a GPU is pure latency (~50 us for 1,472 B).  The relay calls
+// Rijndael from one looper thread per core (relay_local.cpp:475), so calls
+// overlap: they are combined.  A call queues itself; if no batch is running
+// it becomes the leader, takes every queued call (its own included) and runs
+// them as one ragged batch -- one H2D of [schedules | IVs | lists | data],
+// one ragged encrypt and one ragged decrypt with per-call keys and IVs, one
+// D2H -- then wakes the others.  Calls that arrive meanwhile wait and go in
+// the next batch.  A single thread pays no delay: its call leads at once.
 namespace {
 
+struct DropInCall {
+    bool decrypt;
+    const cyaes_key* key;
+    const uint8_t* in;
+    uint8_t* out;
+    uint32_t size;
+    uint8_t* iv;  // nullable, in/out
+    int status = CYAES_OK;
+    bool done = false;
+};
+
 struct DropIn {
-    std::mutex mu;
+    std::mutex mu;  // guards pending / busy; the leader works on the buffers without it
+    std::condition_variable cv;
+    std::vector<DropInCall*> pending;
+    bool busy = false;
+    int init_status = CYAES_OK;
     cyaes_gpu* ctx = nullptr;
     hipStream_t stream = nullptr;
     uint8_t* pinned = nullptr;
     uint64_t pinned_cap = 0;
     uint8_t* d_buf = nullptr;
     uint64_t d_cap = 0;
+    uint64_t batches = 0, calls = 0;  // combined batches and the calls they carried (debugging)
 };
 
 DropIn& dropin() {
@@ -555,32 +581,117 @@ DropIn& dropin() {
     return d;
 }
 
-int dropin_ready(DropIn& d, uint64_t size) {
-    if (!d.ctx) {
-        const char* env = getenv("CYAES_DEVICE");
-        int st = cyaes_gpu_create(env ? atoi(env) : 0, &d.ctx);
-        if (st) return st;
-        DeviceGuard g(d.ctx->device);
-        CY_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-        // The schedule travels with each call's staging copy (no context key table).
-    }
+int dropin_init(DropIn& d) {  // leader only
+    if (d.ctx) return CYAES_OK;
+    const char* env = getenv("CYAES_DEVICE");
+    int st = cyaes_gpu_create(env ? atoi(env) : 0, &d.ctx);
+    if (st) return st;
     DeviceGuard g(d.ctx->device);
-    const uint64_t need_host = 368 + size;
-    if (d.pinned_cap < need_host) {
+    CY_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    return CYAES_OK;
+}
+
+int dropin_reserve(DropIn& d, uint64_t host_bytes, uint64_t dev_bytes) {
+    if (d.pinned_cap < host_bytes) {
         if (d.pinned) CY_TRY(hipHostFree(d.pinned));
         d.pinned = nullptr;
         d.pinned_cap = 0;
-        CY_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.pinned), need_host, hipHostMallocDefault));
-        d.pinned_cap = need_host;
+        const uint64_t cap = std::max<uint64_t>(host_bytes, 2 * d.pinned_cap);
+        CY_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.pinned), cap, hipHostMallocDefault));
+        d.pinned_cap = cap;
     }
-    const uint64_t need_dev = need_host + size;
-    if (d.d_cap < need_dev) {
+    if (d.d_cap < dev_bytes) {
         if (d.d_buf) CY_TRY(hipFree(d.d_buf));
         d.d_buf = nullptr;
         d.d_cap = 0;
-        CY_TRY(hipMalloc(reinterpret_cast<void**>(&d.d_buf), need_dev));
-        d.d_cap = need_dev;
+        const uint64_t cap = std::max<uint64_t>(dev_bytes, 2 * d.d_cap);
+        CY_TRY(hipMalloc(reinterpret_cast<void**>(&d.d_buf), cap));
+        d.d_cap = cap;
     }
+    return CYAES_OK;
+}
+
+// Runs a batch of calls (leader, without the lock).  Image, host and device:
+//   [schedules n x 352][IV in n x 16][offsets n x 8][nbytes n x 4][key index n x 4] | [data in]
+// encrypt calls first, then decrypt calls; device adds [data out] and [IV out n x 16].
+int dropin_batch(DropIn& d, const std::vector<DropInCall*>& calls) {
+    int st = dropin_init(d);
+    if (st) return st;
+    DeviceGuard g(d.ctx->device);
+    std::vector<DropInCall*> order;  // encrypt calls, then decrypt calls
+    order.reserve(calls.size());
+    for (DropInCall* c : calls)
+        if (!c->decrypt) order.push_back(c);
+    const size_t nenc = order.size();
+    for (DropInCall* c : calls)
+        if (c->decrypt) order.push_back(c);
+    const uint64_t n = order.size();
+    const uint64_t o_sched = 0, o_iv = n * 352, o_off = o_iv + n * 16, o_nb = o_off + n * 8, o_kid = o_nb + n * 4;
+    const uint64_t o_data = (o_kid + n * 4 + 255) & ~uint64_t(255);
+    uint64_t data = 0;
+    for (DropInCall* c : order) data += c->size;
+    const uint64_t o_out = (o_data + data + 255) & ~uint64_t(255);
+    const uint64_t o_ivout = o_out + data;  // right after the results: one D2H brings both back
+    st = dropin_reserve(d, o_data + data + n * 16, o_ivout + n * 16);
+    if (st) return st;
+    uint8_t* h = d.pinned;
+    uint64_t* offs = reinterpret_cast<uint64_t*>(h + o_off);
+    uint32_t* nbs = reinterpret_cast<uint32_t*>(h + o_nb);
+    uint32_t* kid = reinterpret_cast<uint32_t*>(h + o_kid);
+    uint64_t pos = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const DropInCall* c = order[i];
+        to_device_schedule(*c->key, reinterpret_cast<uint32_t*>(h + o_sched + 352 * i));
+        memcpy(h + o_iv + 16 * i, c->iv ? c->iv : cyaes_default_iv(), 16);
+        offs[i] = pos;
+        nbs[i] = c->size;
+        kid[i] = (uint32_t)i;
+        memcpy(h + o_data + pos, c->in, c->size);
+        pos += c->size;
+    }
+    CY_TRY(hipMemcpyAsync(d.d_buf, h, o_data + data, hipMemcpyHostToDevice, d.stream));
+    const uint8_t* dd = d.d_buf;
+    const uint32_t* table = reinterpret_cast<const uint32_t*>(dd + o_sched);
+    auto dptr = [&](uint64_t o) { return d.d_buf + o; };
+    // Each direction: calls of one size (the usual relay case, and any single
+    // call) run as a uniform batch -- the flat decrypt spreads even one
+    // payload over the whole GPU -- mixed sizes as a ragged one.
+    for (int dir = 0; dir < 2; dir++) {
+        const uint64_t b0 = dir ? nenc : 0, b1 = dir ? n : nenc;
+        if (b1 == b0) continue;
+        bool same = true;
+        for (uint64_t i = b0 + 1; i < b1; i++) same = same && order[i]->size == order[b0]->size;
+        const uint8_t* in = dptr(o_data) + offs[b0];
+        uint8_t* out = dptr(o_out) + offs[b0];
+        const uint32_t* kidx = reinterpret_cast<const uint32_t*>(dptr(o_kid)) + b0;
+        const uint8_t* ivi = dptr(o_iv) + 16 * b0;
+        uint8_t* ivo = dptr(o_ivout) + 16 * b0;
+        if (same && dir)
+            st = decrypt_uniform(d.ctx, in, out, b1 - b0, order[b0]->size, kidx, 0, ivi, ivo, d.stream, table,
+                                 (uint32_t)n);
+        else if (same)
+            st = encrypt_common(d.ctx, in, out, nullptr, nullptr, b1 - b0, order[b0]->size, kidx, 0, ivi, ivo,
+                                d.stream, table, (uint32_t)n);
+        else if (dir)
+            st = decrypt_ragged(d.ctx, dptr(o_data), dptr(o_out), reinterpret_cast<const uint64_t*>(dptr(o_off)) + b0,
+                                reinterpret_cast<const uint32_t*>(dptr(o_nb)) + b0, b1 - b0, kidx, 0, ivi, ivo,
+                                d.stream, table, (uint32_t)n);
+        else
+            st = encrypt_common(d.ctx, dptr(o_data), dptr(o_out), reinterpret_cast<const uint64_t*>(dptr(o_off)) + b0,
+                                reinterpret_cast<const uint32_t*>(dptr(o_nb)) + b0, b1 - b0, 0, kidx, 0, ivi, ivo,
+                                d.stream, table, (uint32_t)n);
+        if (st) return st;
+    }
+    // results and final chains come back over the input image (no longer needed)
+    CY_TRY(hipMemcpyAsync(h + o_data, dptr(o_out), data + n * 16, hipMemcpyDeviceToHost, d.stream));
+    CY_TRY(hipStreamSynchronize(d.stream));
+    const uint8_t* ivs = h + o_data + data;
+    for (uint64_t i = 0; i < n; i++) {
+        DropInCall* c = order[i];
+        memcpy(c->out, h + o_data + offs[i], c->size);
+        if (c->iv) memcpy(c->iv, ivs + 16 * i, 16);  // cyr_rijndael.cpp:607-608,633-634
+    }
+    (void)dd;
     return CYAES_OK;
 }
 
@@ -589,33 +700,30 @@ int dropin_run(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* o
     if (size == 0) return CYAES_OK;  // no-op, IV unchanged (cyr_rijndael.cpp:600 loop never runs)
     if (size > 0xFFFFFFF0ull) return CYAES_EINVAL;
     DropIn& d = dropin();
-    std::lock_guard<std::mutex> lock(d.mu);
-    int st = dropin_ready(d, size);
-    if (st) return st;
-    DeviceGuard g(d.ctx->device);
-    // Staging image: [schedule 352 B][chain IV 16 B][payload], one H2D copy.
-    uint32_t* sched = reinterpret_cast<uint32_t*>(d.pinned);
-    to_device_schedule(*key, sched);
-    memcpy(d.pinned + 352, iv ? iv : cyaes_default_iv(), 16);
-    memcpy(d.pinned + 368, in, size);
-    uint8_t final_chain[16];
-    if (decrypt && iv) memcpy(final_chain, in + size - 16, 16);  // before an in-place overwrite
-    const uint64_t image = 368 + size;
-    CY_TRY(hipMemcpyAsync(d.d_buf, d.pinned, image, hipMemcpyHostToDevice, d.stream));
-    cyaes_gpu* ctx = d.ctx;
-    const uint32_t* d_sched = reinterpret_cast<const uint32_t*>(d.d_buf);
-    const uint8_t* d_iv = d.d_buf + 352;
-    const uint8_t* d_in = d.d_buf + 368;
-    uint8_t* d_out = d.d_buf + image;
-    st = decrypt ? decrypt_uniform(ctx, d_in, d_out, 1, (uint32_t)size, nullptr, 0, d_iv, nullptr, d.stream, d_sched, 1)
-                 : encrypt_common(ctx, d_in, d_out, nullptr, nullptr, 1, (uint32_t)size, nullptr, 0, d_iv, nullptr,
-                                  d.stream, d_sched, 1);
-    if (st) return st;
-    CY_TRY(hipMemcpyAsync(d.pinned, d_out, size, hipMemcpyDeviceToHost, d.stream));
-    CY_TRY(hipStreamSynchronize(d.stream));
-    memcpy(out, d.pinned, size);
-    if (iv) memcpy(iv, decrypt ? final_chain : out + size - 16, 16);  // cyr_rijndael.cpp:607-608,633-634
-    return CYAES_OK;
+    DropInCall me{decrypt, key, in, out, (uint32_t)size, iv};
+    std::unique_lock<std::mutex> lk(d.mu);
+    d.pending.push_back(&me);
+    while (!me.done) {
+        if (d.busy) {
+            d.cv.wait(lk);
+            continue;
+        }
+        d.busy = true;  // lead: take every queued call, this one included
+        std::vector<DropInCall*> batch;
+        batch.swap(d.pending);
+        lk.unlock();
+        const int st = dropin_batch(d, batch);
+        lk.lock();
+        for (DropInCall* c : batch) {
+            c->status = st;
+            c->done = true;
+        }
+        d.batches++;
+        d.calls += batch.size();
+        d.busy = false;
+        d.cv.notify_all();
+    }
+    return me.status;
 }
 
 }  // namespace
