@@ -121,6 +121,46 @@ def test_dropin_random_roundtrips():
         assert bytes(aes.decrypt(ct)) == data
 
 
+def test_dropin_concurrent_threads():
+    """Synchronous calls from many threads at once are combined into shared GPU
+    batches (mixed directions, sizes, keys, IV in/out, in place): every call
+    still gets exactly its own Rijndael::encrypt/decrypt result."""
+    import threading
+
+    errors = []
+
+    def worker(t):
+        rng = random.Random(100 + t)
+        try:
+            for _ in range(40):
+                key = bytes(rng.randrange(256) for _ in range(16))
+                size = 16 * rng.choice([1, 2, 5, 64, 92, 93, 300])
+                data = bytes(rng.randrange(256) for _ in range(size))
+                aes, ref = ca.Rijndael(key), oracle.Rijndael(key)
+                use_iv = rng.random() < 0.5
+                iv0 = bytes(rng.randrange(256) for _ in range(16))
+                iv, riv = (bytearray(iv0), bytearray(iv0)) if use_iv else (None, None)
+                if rng.random() < 0.5:
+                    got = bytes(aes.encrypt(data, None, size, iv))
+                    want = bytes(ref.encrypt(data, None, size, riv))
+                else:
+                    buf = bytearray(data)  # in place
+                    aes.decrypt(buf, buf, size, iv)
+                    got = bytes(buf)
+                    want = bytes(ref.decrypt(data, None, size, riv))
+                if got != want or iv != riv:
+                    errors.append((t, size, use_iv))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]
+
+
 def test_dropin_config_sizes(golden):
     """Single relay-sized calls (up to the 65280 B relay cap and 64 KiB)."""
     aes = ca.Rijndael(K0)
