@@ -27,7 +27,7 @@ AOBJ     := $(BUILD)/cyaes_adler.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
 .PHONY: all lib mgpu oracle cpptest microbench variant clean
-all: lib mgpu oracle cpptest $(BUILD)/bench_batcher
+all: lib mgpu oracle cpptest $(BUILD)/bench_batcher $(BUILD)/dropin_threads
 lib: $(LIB)
 mgpu: $(MGPU)
 oracle: $(ORACLE)
@@ -61,6 +61,9 @@ $(CPPTEST): tests/cpp/test_rijndael.cpp $(LIB) $(HDRS)
 microbench: $(BUILD)/microbench $(BUILD)/bench_batcher
 
 $(BUILD)/bench_batcher: tools/bench_batcher.cpp $(LIB) $(HDRS) | $(BUILD)
+	$(CXX) -O2 -std=c++17 -Wall -pthread $(INC) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
+
+$(BUILD)/dropin_threads: tools/dropin_threads.cpp $(LIB) $(HDRS) | $(BUILD)
 	$(CXX) -O2 -std=c++17 -Wall -pthread $(INC) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
 
 $(BUILD)/microbench: tools/microbench.hip | $(BUILD)
