@@ -650,8 +650,7 @@ int dropin_batch(DropIn& d, const std::vector<DropInCall*>& calls) {
         pos += c->size;
     }
     CY_TRY(hipMemcpyAsync(d.d_buf, h, o_data + data, hipMemcpyHostToDevice, d.stream));
-    const uint8_t* dd = d.d_buf;
-    const uint32_t* table = reinterpret_cast<const uint32_t*>(dd + o_sched);
+    const uint32_t* table = reinterpret_cast<const uint32_t*>(d.d_buf + o_sched);
     auto dptr = [&](uint64_t o) { return d.d_buf + o; };
     // Each direction: calls of one size (the usual relay case, and any single
     // call) run as a uniform batch -- the flat decrypt spreads even one
@@ -691,7 +690,6 @@ int dropin_batch(DropIn& d, const std::vector<DropInCall*>& calls) {
         memcpy(c->out, h + o_data + offs[i], c->size);
         if (c->iv) memcpy(c->iv, ivs + 16 * i, 16);  // cyr_rijndael.cpp:607-608,633-634
     }
-    (void)dd;
     return CYAES_OK;
 }
 
