@@ -561,18 +561,25 @@ struct DropInCall {
     bool done = false;
 };
 
-struct DropIn {
-    std::mutex mu;  // guards pending / busy; the leader works on the buffers without it
-    std::condition_variable cv;
-    std::vector<DropInCall*> pending;
+// Staging of one batch in flight.  Two slots: while one batch runs on the
+// GPU the next leader gathers and launches the calls queued meanwhile, so
+// latency-bound batches (a few chains each) overlap on the device.
+struct DropInSlot {
     bool busy = false;
-    int init_status = CYAES_OK;
-    cyaes_gpu* ctx = nullptr;
     hipStream_t stream = nullptr;
     uint8_t* pinned = nullptr;
     uint64_t pinned_cap = 0;
     uint8_t* d_buf = nullptr;
     uint64_t d_cap = 0;
+};
+constexpr int kDropInSlots = 2;
+
+struct DropIn {
+    std::mutex mu;  // guards pending, slot ownership and init; a leader works on its slot without it
+    std::condition_variable cv;
+    std::vector<DropInCall*> pending;
+    cyaes_gpu* ctx = nullptr;
+    DropInSlot slots[kDropInSlots];
     uint64_t batches = 0, calls = 0;  // combined batches and the calls they carried (debugging)
 };
 
@@ -581,17 +588,27 @@ DropIn& dropin() {
     return d;
 }
 
-int dropin_init(DropIn& d) {  // leader only
+int dropin_init(DropIn& d) {  // under d.mu
     if (d.ctx) return CYAES_OK;
     const char* env = getenv("CYAES_DEVICE");
-    int st = cyaes_gpu_create(env ? atoi(env) : 0, &d.ctx);
+    cyaes_gpu* ctx = nullptr;
+    int st = cyaes_gpu_create(env ? atoi(env) : 0, &ctx);
     if (st) return st;
-    DeviceGuard g(d.ctx->device);
-    CY_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    DeviceGuard g(ctx->device);
+    for (DropInSlot& sl : d.slots) {
+        const hipError_t e = hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            for (DropInSlot& s2 : d.slots)
+                if (s2.stream) (void)hipStreamDestroy(s2.stream), s2.stream = nullptr;
+            cyaes_gpu_destroy(ctx);
+            return map_err(e);
+        }
+    }
+    d.ctx = ctx;
     return CYAES_OK;
 }
 
-int dropin_reserve(DropIn& d, uint64_t host_bytes, uint64_t dev_bytes) {
+int dropin_reserve(DropInSlot& d, uint64_t host_bytes, uint64_t dev_bytes) {
     if (d.pinned_cap < host_bytes) {
         if (d.pinned) CY_TRY(hipHostFree(d.pinned));
         d.pinned = nullptr;
@@ -614,10 +631,9 @@ int dropin_reserve(DropIn& d, uint64_t host_bytes, uint64_t dev_bytes) {
 // Runs a batch of calls (leader, without the lock).  Image, host and device:
 //   [schedules n x 352][IV in n x 16][offsets n x 8][nbytes n x 4][key index n x 4] | [data in]
 // encrypt calls first, then decrypt calls; device adds [data out] and [IV out n x 16].
-int dropin_batch(DropIn& d, const std::vector<DropInCall*>& calls) {
-    int st = dropin_init(d);
-    if (st) return st;
-    DeviceGuard g(d.ctx->device);
+int dropin_batch(cyaes_gpu* ctx, DropInSlot& d, const std::vector<DropInCall*>& calls) {
+    int st = CYAES_OK;
+    DeviceGuard g(ctx->device);
     std::vector<DropInCall*> order;  // encrypt calls, then decrypt calls
     order.reserve(calls.size());
     for (DropInCall* c : calls)
@@ -666,17 +682,17 @@ int dropin_batch(DropIn& d, const std::vector<DropInCall*>& calls) {
         const uint8_t* ivi = dptr(o_iv) + 16 * b0;
         uint8_t* ivo = dptr(o_ivout) + 16 * b0;
         if (same && dir)
-            st = decrypt_uniform(d.ctx, in, out, b1 - b0, order[b0]->size, kidx, 0, ivi, ivo, d.stream, table,
+            st = decrypt_uniform(ctx, in, out, b1 - b0, order[b0]->size, kidx, 0, ivi, ivo, d.stream, table,
                                  (uint32_t)n);
         else if (same)
-            st = encrypt_common(d.ctx, in, out, nullptr, nullptr, b1 - b0, order[b0]->size, kidx, 0, ivi, ivo,
+            st = encrypt_common(ctx, in, out, nullptr, nullptr, b1 - b0, order[b0]->size, kidx, 0, ivi, ivo,
                                 d.stream, table, (uint32_t)n);
         else if (dir)
-            st = decrypt_ragged(d.ctx, dptr(o_data), dptr(o_out), reinterpret_cast<const uint64_t*>(dptr(o_off)) + b0,
+            st = decrypt_ragged(ctx, dptr(o_data), dptr(o_out), reinterpret_cast<const uint64_t*>(dptr(o_off)) + b0,
                                 reinterpret_cast<const uint32_t*>(dptr(o_nb)) + b0, b1 - b0, kidx, 0, ivi, ivo,
                                 d.stream, table, (uint32_t)n);
         else
-            st = encrypt_common(d.ctx, dptr(o_data), dptr(o_out), reinterpret_cast<const uint64_t*>(dptr(o_off)) + b0,
+            st = encrypt_common(ctx, dptr(o_data), dptr(o_out), reinterpret_cast<const uint64_t*>(dptr(o_off)) + b0,
                                 reinterpret_cast<const uint32_t*>(dptr(o_nb)) + b0, b1 - b0, 0, kidx, 0, ivi, ivo,
                                 d.stream, table, (uint32_t)n);
         if (st) return st;
@@ -700,17 +716,25 @@ int dropin_run(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* o
     DropIn& d = dropin();
     DropInCall me{decrypt, key, in, out, (uint32_t)size, iv};
     std::unique_lock<std::mutex> lk(d.mu);
+    const int ist = dropin_init(d);
+    if (ist) return ist;
     d.pending.push_back(&me);
     while (!me.done) {
-        if (d.busy) {
+        DropInSlot* slot = nullptr;
+        for (DropInSlot& sl : d.slots)
+            if (!sl.busy) {
+                slot = &sl;
+                break;
+            }
+        if (!slot || d.pending.empty()) {  // both slots in flight, or this call already taken by a leader
             d.cv.wait(lk);
             continue;
         }
-        d.busy = true;  // lead: take every queued call, this one included
+        slot->busy = true;  // lead: take every queued call (this one, if still queued, included)
         std::vector<DropInCall*> batch;
         batch.swap(d.pending);
         lk.unlock();
-        const int st = dropin_batch(d, batch);
+        const int st = dropin_batch(d.ctx, *slot, batch);
         lk.lock();
         for (DropInCall* c : batch) {
             c->status = st;
@@ -718,7 +742,7 @@ int dropin_run(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* o
         }
         d.batches++;
         d.calls += batch.size();
-        d.busy = false;
+        slot->busy = false;
         d.cv.notify_all();
     }
     return me.status;
