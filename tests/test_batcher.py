@@ -71,6 +71,53 @@ def test_mixed_requests_from_threads_match_oracle(batcher):
         batcher.session_close(s)
 
 
+def test_session_churn_while_submitting(batcher):
+    """Submitters read a per-thread snapshot of the session table, refreshed
+    when an open or close bumps its version.  Each worker keeps reopening its
+    own session with a new key while the others do the same, and submits in
+    between: every request must use the key its slot held when it was
+    submitted, and a submit to a closed slot must fail with CYAES_ERANGE."""
+    results = []
+    lock = threading.Lock()
+    errors = []
+
+    def worker(tid):
+        rng = random.Random(500 + tid)
+        try:
+            for rnd in range(12):
+                key = bytes(rng.randrange(256) for _ in range(16))
+                slot = batcher.session_open(key)
+                for _ in range(rng.randrange(1, 12)):
+                    size = 16 * rng.choice([1, 7, 92, 300])
+                    data = bytes(rng.randrange(256) for _ in range(size))
+                    out = bytearray(size)
+                    rec = {"key": key, "data": data, "out": out, "status": None}
+
+                    def done(status, rec=rec):
+                        rec["status"] = status
+                    batcher.submit(ca.OP_ENCRYPT, slot, data, out, size, done)
+                    with lock:
+                        results.append(rec)
+                batcher.session_close(slot)
+                try:  # the slot is closed now (another thread may reopen it: then it is theirs)
+                    batcher.submit(ca.OP_ENCRYPT, slot, b"\0" * 16, bytearray(16), 16, None)
+                except ca.CyaesError as e:
+                    assert e.status == ca.CYAES_ERANGE
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors[:3]
+    assert batcher.flush() == ca.CYAES_OK
+    for r in results:
+        assert r["status"] == ca.CYAES_OK
+        assert bytes(r["out"]) == bytes(oracle.Rijndael(r["key"]).encrypt(bytearray(r["data"])))
+
+
 def test_relay_seal_open_round_trip(batcher):
     """SEAL = relay_local.cpp:189-206 (packet + 0xCE pad + encrypt); OPEN =
     relay_server.cpp:329 (decrypt in place)."""
