@@ -944,6 +944,13 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                     const uint64_t of = rlane64(offh, j);
                     rr[k] = (uint32_t)(g - bs);  // < 2^28: within one payload
                     orow[k] = of + 16ull * rr[k];
+                } else if (jhi == j + 1) {  // two payloads (most rows of MTU-sized packets): scalar reads, one select
+                    const uint64_t bs0 = rlane64(bsh, j), bs1 = rlane64(bsh, jhi);
+                    const uint64_t of0 = rlane64(offh, j), of1 = rlane64(offh, jhi);
+                    const bool second = g >= bs1;
+                    rr[k] = (uint32_t)(g - (second ? bs1 : bs0));
+                    orow[k] = (second ? of1 : of0) + 16ull * rr[k];
+                    j = second ? jhi : j;
                 } else {  // largest j in [jlo, jhi] with bs_j <= g (an empty payload never wins)
                     uint32_t hi = jhi;
                     const int steps = 32 - __builtin_clz(jhi - j);
@@ -967,8 +974,10 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                 const uint64_t p = p0 + jr[k];
                 if (valid[k] && rr[k] == 0)
                     pv[k] = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
-                const uint32_t nbj = bperm(nbh, jr[k]);  // all lanes: a bpermute from an inactive lane reads 0
-                if (a.iv_out && valid[k] && rr[k] + 1 == nbj) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+                if (a.iv_out) {  // (uniform branch: every lane runs the bpermute; one from an inactive lane reads 0)
+                    const uint32_t nbj = bperm(nbh, jr[k]);
+                    if (valid[k] && rr[k] + 1 == nbj) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+                }
             }
             if (!KEYED) {
                 dec_cbc<R>(lds, lo, dk0, c, pv);

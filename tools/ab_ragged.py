@@ -5,7 +5,7 @@ Relay traffic in HBM is ragged (cyaes_relay.h: packets with 12-B headers);
 this times cyaes_gpu_{en,de}crypt_ragged on N equal payloads laid out
 contiguously (offsets = p * size) against the uniform entry points, and on a
 relay-packet stream layout (payload at packet offset 12, 4-B aligned).
-usage: python tools/ab_ragged.py [--rounds 5]"""
+usage: python tools/ab_ragged.py [--rounds 5] [--lib build/variants/x.so]"""
 import argparse
 import os
 import statistics
@@ -18,14 +18,19 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--lib", default=None, help="a variant libcyaes.so (make variant)")
+    ap.add_argument("--sizes", default=None, help="n:pb,... (default: the four below)")
     args = ap.parse_args()
     import numpy as np
     import torch
     import cyclone_amd as ca
-    c = ca.GpuContext(0)
+    c = ca.GpuContext(0, lib=ca.load_library(os.path.abspath(args.lib)) if args.lib else None)
     c.set_keys(bytes(range(16)))
     s = torch.cuda.current_stream()
-    for n, pb in ((21000, 1472), (262144, 1472), (1048576, 1472), (65536, 65280)):
+    sizes = ((21000, 1472), (262144, 1472), (1048576, 1472), (65536, 65280))
+    if args.sizes:
+        sizes = tuple(tuple(int(v) for v in x.split(":")) for x in args.sizes.split(","))
+    for n, pb in sizes:
         nbytes = n * pb
         pt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
         c.fill_synthetic(pt, 0, n, pb, 0x5EEDC1C1)
