@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <mutex>
+#include <new>
 #include <vector>
 
 #include "cyaes.h"
@@ -734,7 +735,12 @@ int dropin_run(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* o
         std::vector<DropInCall*> batch;
         batch.swap(d.pending);
         lk.unlock();
-        const int st = dropin_batch(d.ctx, *slot, batch);
+        int st;
+        try {
+            st = dropin_batch(d.ctx, *slot, batch);
+        } catch (const std::bad_alloc&) {  // the slot and the waiters must still be released
+            st = CYAES_ENOMEM;
+        }
         lk.lock();
         for (DropInCall* c : batch) {
             c->status = st;
