@@ -18,7 +18,7 @@ import cyclone_amd as ca
 import oracle
 
 pytestmark = pytest.mark.gpu
-NCASES = 160
+NCASES = int(os.environ.get("CYAES_SWEEP_CASES", "160"))  # soak runs raise it
 
 
 @pytest.fixture(scope="module")
