@@ -315,8 +315,14 @@ __device__ __forceinline__ void prio_feedback(uint32_t* lead, uint32_t step, uin
     else __builtin_amdgcn_s_setprio(0);
 #endif
 }
-constexpr uint32_t kEncPrioDiv = 4;  // steps = 8-block chunks (A/B: 1, 2, 4, 8 -> 4 best)
-constexpr uint32_t kDecPrioDiv = 8;  // steps = 64*kDecRows-block rows (A/B: 4, 8, 16 -> 8)
+#ifndef CYAES_ENC_PRIO_DIV
+#define CYAES_ENC_PRIO_DIV 4
+#endif
+#ifndef CYAES_DEC_PRIO_DIV
+#define CYAES_DEC_PRIO_DIV 8
+#endif
+constexpr uint32_t kEncPrioDiv = CYAES_ENC_PRIO_DIV;  // steps = 8-block chunks (A/B: 1, 2, 4, 8 -> 4 best)
+constexpr uint32_t kDecPrioDiv = CYAES_DEC_PRIO_DIV;  // steps = 64*kDecRows-block rows (A/B: 4, 8, 16 -> 8)
 
 
 // 16-B block at a 4-byte-aligned address (ragged batches: relay packets put
