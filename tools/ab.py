@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--payloads", type=int, default=262144)
     ap.add_argument("--payload-bytes", type=int, default=65536)
     ap.add_argument("--ppk", type=int, default=0, help="payloads per session key (0: one key)")
+    ap.add_argument("--key-idx", action="store_true", help="with --ppk: the same sessions as a per-payload index array")
     args = ap.parse_args()
     import torch
     import cyclone_amd as ca
@@ -44,6 +45,9 @@ def main():
     rt = torch.empty_like(pt)
     ctxs[0].fill_synthetic(pt, 0, n, pb, 0x5EEDC1C1)
     s = torch.cuda.current_stream()
+    kidx = None
+    if args.key_idx and args.ppk:
+        kidx = (torch.arange(n, dtype=torch.int64, device="cuda") // args.ppk).to(torch.int32)
     times = {p: {"enc": [], "dec": []} for p in args.libs}
     probes = {}
     digests = {}
@@ -51,9 +55,11 @@ def main():
         for path, c in zip(args.libs, ctxs):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record(s)
-            c.encrypt_uniform(pt, ct, n, pb, payloads_per_key=args.ppk, stream=s.cuda_stream)
+            c.encrypt_uniform(pt, ct, n, pb, key_idx=kidx, payloads_per_key=0 if kidx is not None else args.ppk,
+                              stream=s.cuda_stream)
             e[1].record(s)
-            c.decrypt_uniform(ct, rt, n, pb, payloads_per_key=args.ppk, stream=s.cuda_stream)
+            c.decrypt_uniform(ct, rt, n, pb, key_idx=kidx, payloads_per_key=0 if kidx is not None else args.ppk,
+                              stream=s.cuda_stream)
             e[2].record(s)
             torch.cuda.synchronize()
             if r == 0:  # warm-up round; check outputs
