@@ -13,7 +13,10 @@ HOSTFLAGS:= -O2 -std=c++17 -fPIC -Wall $(INC) -D__HIP_PLATFORM_AMD__ -I/opt/rocm
 LIB      := cyclone_amd/libcyaes.so
 MGPU     := cyclone_amd/libcyaes_mgpu.so
 ORACLE   := oracle/liboracle.so
-CPPTEST  := $(BUILD)/test_rijndael
+CPPTEST  := $(BUILD)/test_rijndael $(BUILD)/relay_calls
+# Measurement-only build of the same kernels with the in-kernel clock probe
+# (CYAES_CLOCK_PROBE): bench.py reads the shader clock under load from it.
+PROBE    := $(BUILD)/variants/clockprobe.so
 
 KSRC     := cyclone_amd/csrc/cyaes_kernels.hip
 ASRC     := cyclone_amd/csrc/cyaes_adler.hip
@@ -26,12 +29,13 @@ KOBJ     := $(BUILD)/cyaes_kernels.o
 AOBJ     := $(BUILD)/cyaes_adler.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
-.PHONY: all lib mgpu oracle cpptest microbench variant clean
-all: lib mgpu oracle cpptest $(BUILD)/bench_batcher $(BUILD)/dropin_threads
+.PHONY: all lib mgpu oracle cpptest probe microbench variant clean
+all: lib mgpu oracle cpptest probe $(BUILD)/bench_batcher $(BUILD)/dropin_threads
 lib: $(LIB)
 mgpu: $(MGPU)
 oracle: $(ORACLE)
 cpptest: $(CPPTEST)
+probe: $(PROBE)
 
 $(BUILD):
 	mkdir -p $(BUILD)
@@ -55,8 +59,12 @@ $(MGPU): cyclone_amd/csrc/cyaes_mgpu.cpp include/cyaes_mgpu.h $(LIB)
 $(ORACLE): oracle/aes_oracle.c
 	$(CC) -O2 -fPIC -shared -pthread -Wall -o $@ $<
 
-$(CPPTEST): tests/cpp/test_rijndael.cpp $(LIB) $(HDRS)
+$(BUILD)/test_rijndael: tests/cpp/test_rijndael.cpp $(LIB) $(HDRS) | $(BUILD)
 	$(CXX) -O2 -std=c++17 -Wall $(INC) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
+
+# The relay's Rijndael call expressions, verbatim; -DNDEBUG as a release build
+$(BUILD)/relay_calls: tests/cpp/relay_calls.cpp $(LIB) $(HDRS) | $(BUILD)
+	$(CXX) -O2 -DNDEBUG -std=c++17 -Wall -Wno-misleading-indentation $(INC) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
 
 microbench: $(BUILD)/microbench $(BUILD)/bench_batcher
 
@@ -68,6 +76,11 @@ $(BUILD)/dropin_threads: tools/dropin_threads.cpp $(LIB) $(HDRS) | $(BUILD)
 
 $(BUILD)/microbench: tools/microbench.hip | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
+
+$(PROBE): $(KSRC) $(HDRS) $(HOBJ) $(AOBJ)
+	mkdir -p $(BUILD)/variants
+	$(HIPCC) $(HIPFLAGS) -DCYAES_CLOCK_PROBE=1 -c $(KSRC) -o $(BUILD)/variants/clockprobe.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(BUILD)/variants/clockprobe.o $(AOBJ) $(HOBJ)
 
 # A/B variants: make variant NAME=x DEFS="-DFOO=1" -> build/variants/x.so
 variant: $(HOBJ) $(AOBJ) | $(BUILD)

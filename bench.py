@@ -2,29 +2,45 @@
 """bench.py -- device-resident AES-128-CBC encrypt+decrypt throughput on MI355X.
 
 Metric (BASELINE.json): "AES encrypt+decrypt GiB/s device-resident (64 KiB
-payloads); % HBM roofline @1/2/4/8 GPU".  One step = one CBC-encrypt pass
-plus one CBC-decrypt pass over the per-GPU batch (config C of BASELINE.json:
-1 key, 262,144 payloads x 65,536 B = 16 GiB per GPU; every payload an
-independent chain from DefaultIV, the relay semantics of
-relay_local.cpp:206 / relay_server.cpp:329).  value = 2 x bytes x steps x
-ranks / max-over-ranks wall time, in GiB/s (2^30).
+payloads); % HBM roofline @1/2/4/8 GPU".  Every payload is an independent
+CBC chain from DefaultIV (the relay semantics of relay_local.cpp:206 /
+relay_server.cpp:329,472).
+
+Headline workload (default `--config E`, BASELINE.json configs[4], SURVEY.md
+§8(d)): 8,388,608 payloads x 65,536 B = 512 GiB in total, processed in 32
+fixed passes of 262,144 payloads (16 GiB, exactly config C's batch).  At N
+GPUs, GPU g walks passes [g*32/N, (g+1)*32/N): the total is fixed and the
+per-GPU pass size is the same at every N.  One step = one
+walk of the whole E job: for each pass of the rank, the plaintext is written
+into HBM (untimed: input staging, `fill_ms`), then one encrypt pass and one
+decrypt pass run on it, timed between device synchronisations.
+value = 2 x 512 GiB x steps / max over ranks of the summed timed seconds.
+At N = 1 the rank walks all 32 passes, so the pass roofline is config C's.
 
 Multi-GPU (torchrun, one process per GPU): rank 0 holds the session key and
-broadcasts it over RCCL (xGMI); every rank expands it on its device and
-processes its own payload shard (weak scaling: per-GPU batch fixed, payload
-indices [rank*P, (rank+1)*P) of the global stream).  No data-path collective.
+broadcasts it over RCCL (xGMI); every rank expands it on its device and walks
+its own passes.  No data-path collective.
 
-packet_configs: the north star's other named sizes, measured after the
-headline config at the same GPU count with the same timing rules: config B
-(1 M x 1,472 B, MTU-sized) and config D (4,096 session keys x 256 x 1,472 B).
-Reported beside `value`, never as it.
+`--config A|B|C|D` run one BASELINE.json config per GPU instead (weak
+scaling: per-GPU batch fixed, payload range [rank*P, (rank+1)*P)).
+packet_configs: configs B (1 M x 1,472 B) and D (4,096 session keys x 256 x
+1,472 B), measured after the headline at the same GPU count with the same
+timing rules; reported beside `value`, never as it.
+
+roofline: the kernels are bound by LDS gather issue, so
+`bound` is "lds"; `frac` keeps the contract's definition (algorithmic bytes /
+kernel time / 8 TB/s) and `ceiling` prices the binding unit: lookups per
+clock per CU at the shader clock measured inside the kernels (a clock-probe
+build of the same kernels, build/variants/clockprobe.so).
 
 cpu_baseline: the oracle (a plain-C restatement of the reference's scalar
-Rijndael, oracle/aes_oracle.c) timed on this host's cores on a bounded
+Rijndael, oracle/aes_oracle.c) on every usable host core (relay's
+work_thread_counts = get_cpu_counts(), relay_local.cpp:475) on a bounded
 sample of the same workload, rank 0 at N=1 only.
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -34,9 +50,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "AES encrypt+decrypt GiB/s device-resident (64 KiB payloads); % HBM roofline @1/2/4/8 GPU"
 LOOKUPS_PER_BLOCK = 160      # 9 x 16 T-table + 16 S-box lookups (cyr_rijndael.cpp:659-704)
-LDS_LANES_PER_CLK_CU = 32    # ds_read_b32: 2 x 32-lane groups, 1 cycle each (MI355X_MICROARCH.md, LDS)
+LDS_LANES_PER_CLK_CU = 32    # ds_read_b32: 2 cycles per wave64 instruction (MI355X_MICROARCH.md, LDS)
+LDS_MEASURED_PEAK = 27.7     # back-to-back conflict-free ds_read_b32 microbench (profiles/r01/microbench.jsonl)
 NUM_CUS = 256
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+HBM_COPY_CEILING_GBS = 6290.0  # measured float4 copy ceiling, same guide
 PLAINTEXT_SEED = 0x5EEDC1C1
 CONFIGS = {
     # name: (payloads per GPU, payload bytes, payloads per session key (0 = one key))
@@ -45,6 +63,7 @@ CONFIGS = {
     "D": (1048576, 1472, 256),
     "A": (4096, 1024, 0),
 }
+E_PASS_PAYLOADS, E_PASSES, E_PAYLOAD_BYTES = 262144, 32, 65536  # 32 x 2^18 = 2^23 payloads
 
 
 def log(*a):
@@ -56,22 +75,25 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C", choices=sorted(CONFIGS))
-    ap.add_argument("--payloads", type=int, default=0, help="override payloads per GPU")
+    ap.add_argument("--config", default="E", choices=sorted(CONFIGS) + ["E"])
+    ap.add_argument("--payloads", type=int, default=0, help="A-D: override payloads per GPU")
+    ap.add_argument("--e-pass-payloads", type=int, default=E_PASS_PAYLOADS, help="E: payloads per pass")
+    ap.add_argument("--e-passes", type=int, default=E_PASSES, help="E: passes in the whole job")
     ap.add_argument("--cpu-sample", type=int, default=0, help="cpu baseline sample payloads (0 = auto)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-clock", action="store_true", help="skip the in-kernel clock measurement")
     ap.add_argument("--packet-configs", default="B,D",
                     help="other BASELINE.json packet configs measured after the headline one ('none' to skip)")
     ap.add_argument("--packet-steps", type=int, default=20)
     ap.add_argument("--packet-warmup", type=int, default=20,
                     help="untimed steps before each packet config (a 1,472-B step is ~2 ms; 20 cover the clock "
-                         "ramp that 2 steps of the 23-ms headline step cover, profiles/r01/packet_warmup.txt)")
+                         "ramp, profiles/r01/packet_warmup.txt)")
     return ap.parse_args()
 
 
 def session_keys(n):
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    """Config D session keys: LE(splitmix64(S+2s)) || LE(splitmix64(S+2s+1))."""
     import struct
     seed = 0xC1C10E55D0000000
 
@@ -83,14 +105,32 @@ def session_keys(n):
     return b"".join(struct.pack("<QQ", sm(seed + 2 * s), sm(seed + 2 * s + 1)) for s in range(n))
 
 
+def usable_cores():
+    """(threads to use, facts): the CPUs this process may run on -- the affinity
+    mask, capped by a cgroup CPU quota when one is set (a GPU box shares its
+    host; nproc / os.cpu_count() show the whole machine)."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    use = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return use, {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota}
+
+
 def cpu_baseline(cfg_name, npay, pb, ppk, d_ct, torch, sample=0):
-    """Oracle (scalar reference restatement) on the host cores; bounded sample."""
+    """Oracle (scalar reference restatement) on the usable host cores; bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
-    # ~4 GiB of payload by default: ~20 s of CPU work over 16 threads
-    sample = min(npay, sample if sample > 0 else int(max(1, (4 << 30) // pb)))
+    threads, facts = usable_cores()
+    # ~0.4 GiB of payload per thread (at most 8 GiB): ~2-4 s of CPU time per thread at ~0.2 GiB/s/core
+    # per direction, a few seconds of wall time
+    sample = min(npay, sample if sample > 0 else int(max(1, min(threads * (400 << 20), 8 << 30) // pb)))
     keys = [bytes(range(16))] if not ppk else [session_keys(sample // ppk + 1)[16 * s:16 * s + 16]
                                               for s in range(sample // ppk + 1)]
     pt = oracle.synthetic(0, sample, pb)
@@ -100,7 +140,7 @@ def cpu_baseline(cfg_name, npay, pb, ppk, d_ct, torch, sample=0):
     rt = oracle.batch(True, keys, ppk, ct, pb, nthreads=threads)
     t2 = time.perf_counter()
     # single-core figure on a smaller slice
-    s1 = max(1, sample // 32)
+    s1 = max(1, min(sample, (256 << 20) // pb))
     t3 = time.perf_counter()
     ct1 = oracle.batch(False, keys, ppk, pt[:s1 * pb], pb, nthreads=1)
     t4 = time.perf_counter()
@@ -110,18 +150,18 @@ def cpu_baseline(cfg_name, npay, pb, ppk, d_ct, torch, sample=0):
     gpu_sample = d_ct[: sample * pb].cpu().numpy()
     exact = bool(np.array_equal(gpu_sample, ct)) and bool(np.array_equal(rt, pt))
     gib = float(1 << 30)
-    return {
+    return dict({
         "value": round(2 * sample * pb / (t2 - t0) / gib, 4),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": "config %s: first %d payloads x %d B (%.2f GiB), encrypt then decrypt, %d threads "
-                  "(one Rijndael key schedule per thread, as relay's work threads); oracle/aes_oracle.c"
-                  % (cfg_name, sample, pb, sample * pb / gib, threads),
+        "sample": "config %s: first %d payloads x %d B (%.2f GiB), encrypt then decrypt, %d threads = the usable "
+                  "host cores (one Rijndael key schedule per thread, as relay's work threads, relay_local.cpp:475); "
+                  "oracle/aes_oracle.c" % (cfg_name, sample, pb, sample * pb / gib, threads),
         "single_core": round(2 * s1 * pb / ((t4 - t3) + (t5 - t4)) / gib, 4),
         "seconds": round(t2 - t0, 3),
         "matches_gpu": exact,
-    }
+    }, **facts)
 
 
 def main():
@@ -154,21 +194,38 @@ def main():
     golden = json.load(open(os.path.join(ROOT, "tests", "golden", "openssl_vectors.json")))["configs"]
     gib = float(1 << 30)
 
-    def run_config(name, npay, steps, warmup, verify, keep_cipher=False):
-        """One config, timed as the contract says; returns a result dict (rank-local
-        kernel times, max-over-ranks wall time)."""
-        _, pb, ppk = CONFIGS[name]
-        nbytes = npay * pb
+    def max_over_ranks(x):
+        v = torch.tensor([x], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        return float(v.item())
+
+    def all_ok(ok):
+        flag = torch.tensor([0 if ok else 1], device="cuda")
+        if world > 1:
+            dist.all_reduce(flag)
+        return int(flag.item()) == 0
+
+    def set_session_keys(p0, npay, ppk):
         # Session key(s): rank 0 owns them (the relay's DH secret), RCCL-broadcast
         # over xGMI straight into device memory; each GPU expands its own sessions.
-        p0, npay = cdist.weak_shard(npay, rank)
         nkeys = cdist.session_range(0, npay * world, ppk)[1]
         d_keys = cdist.broadcast_keys((session_keys(nkeys) if ppk else bytes(range(16))) if rank == 0 else None,
                                       nkeys, "cuda")
         k0, nk = cdist.session_range(p0, npay, ppk)
-        d_keys = d_keys[16 * k0: 16 * (k0 + nk)].contiguous()
-        ctx.set_keys_device(d_keys, nk, sh)
+        ctx.set_keys_device(d_keys[16 * k0: 16 * (k0 + nk)].contiguous(), nk, sh)
 
+    def digests_match(g, d_pt, d_ct, nbytes):
+        return (["%016x" % v for v in ctx.digest(d_ct, nbytes, sh)] == g["cipher_digest"] and
+                ["%016x" % v for v in ctx.digest(d_pt, nbytes, sh)] == g["plain_digest"])
+
+    def run_config(name, npay, steps, warmup, verify, keep_cipher=False):
+        """One config of A-D, timed as the contract says; returns a result dict
+        (rank-local kernel times, max-over-ranks wall time)."""
+        _, pb, ppk = CONFIGS[name]
+        nbytes = npay * pb
+        p0, npay = cdist.weak_shard(npay, rank)
+        set_session_keys(p0, npay, ppk)
         log("rank %d/%d: config %s, %d payloads x %d B = %.2f GiB per GPU, %d CUs"
             % (rank, world, name, npay, pb, nbytes / 2**30, ctx.num_cus))
         d_pt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -189,20 +246,12 @@ def main():
 
         parity = None
         if verify:
-            gname = name if rank == 0 else ("E_rank1" if (rank == 1 and name == "C") else None)
-            dp = ctx.digest(d_pt, nbytes, sh)
-            dc = ctx.digest(d_ct, nbytes, sh)
-            dr = ctx.digest(d_rt, nbytes, sh)
-            ok = dr == dp
-            g = golden.get(gname) if gname else None
+            ok = ctx.digest(d_rt, nbytes, sh) == ctx.digest(d_pt, nbytes, sh)
+            g = golden.get(name) if rank == 0 else None
             if g and g["npayloads"] == npay and g["payload_bytes"] == pb and g["p0"] == p0:
-                ok = ok and ["%016x" % v for v in dc] == g["cipher_digest"] and \
-                    ["%016x" % v for v in dp] == g["plain_digest"]
+                ok = ok and digests_match(g, d_pt, d_ct, nbytes)
             ok = ok and ctx.check() == ca.CYAES_OK
-            flag = torch.tensor([0 if ok else 1], device="cuda")
-            if world > 1:
-                dist.all_reduce(flag)
-            parity = "bit-exact" if int(flag.item()) == 0 else "MISMATCH"
+            parity = "bit-exact" if all_ok(ok) else "MISMATCH"
             log("config %s parity: %s" % (name, parity))
 
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
@@ -221,50 +270,180 @@ def main():
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
-        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
-        if world > 1:
-            dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        t = float(elapsed.item())
+        t = max_over_ranks(t1 - t0)
         res = {
             "name": name, "npay": npay, "pb": pb, "ppk": ppk, "nbytes": nbytes, "t": t, "steps": steps,
             "value": 2.0 * nbytes * steps * world / t / gib,
             "enc_ms": sum(a.elapsed_time(b) for a, b, _ in ev) / steps,
             "dec_ms": sum(b.elapsed_time(c) for _, b, c in ev) / steps,
-            "parity": parity, "d_ct": d_ct if keep_cipher else None,
+            "parity": parity, "d_ct": d_ct if keep_cipher else None, "d_pt": d_pt if keep_cipher else None,
         }
-        del d_pt, d_rt
+        del d_rt
         if not keep_cipher:
-            del d_ct
+            del d_ct, d_pt
         return res
 
-    npay = args.payloads or CONFIGS[args.config][0]
-    main_res = run_config(args.config, npay, args.steps, args.warmup, not args.no_verify, keep_cipher=True)
+    def run_e(steps, warmup, verify):
+        """Config E: the whole job's fixed passes, this rank's share (see module doc)."""
+        pp, passes, pb = args.e_pass_payloads, args.e_passes, E_PAYLOAD_BYTES
+        if passes % world:
+            raise SystemExit("config E: %d passes do not split over %d ranks" % (passes, world))
+        mine = list(range(rank * passes // world, (rank + 1) * passes // world))
+        nbytes = pp * pb
+        set_session_keys(0, pp, 0)
+        log("rank %d/%d: config E, passes %d..%d of %d, %d payloads x %d B = %.2f GiB per pass, %d CUs"
+            % (rank, world, mine[0], mine[-1], passes, pp, pb, nbytes / gib, ctx.num_cus))
+        d_pt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        d_ct = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        d_rt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        gfile = os.path.join(ROOT, "tests", "golden", "config_e_passes.json")
+        gpass = {}
+        if os.path.exists(gfile):
+            for layout in json.load(open(gfile)).values():
+                if isinstance(layout, dict) and layout.get("pass_payloads") == pp:
+                    gpass = {g["pass"]: g for g in layout["passes"]}
+
+        def fill(i):
+            ctx.fill_synthetic(d_pt, i * pp, pp, pb, PLAINTEXT_SEED, sh)
+
+        def enc():
+            ctx.encrypt_uniform(d_pt, d_ct, pp, pb, stream=sh)
+
+        def dec():
+            ctx.decrypt_uniform(d_ct, d_rt, pp, pb, stream=sh)
+
+        verified, ok = [], True
+        for w in range(max(warmup, 1 if verify else 0)):
+            for i in mine:
+                fill(i)
+                enc()
+                dec()
+                if verify and w == 0:
+                    good = ctx.digest(d_rt, nbytes, sh) == ctx.digest(d_pt, nbytes, sh)
+                    if i in gpass:
+                        good = good and digests_match(gpass[i], d_pt, d_ct, nbytes)
+                        if good:
+                            verified.append(i)
+                    ok = ok and good
+        torch.cuda.synchronize()
+        parity = None
+        if verify:
+            ok = ok and ctx.check() == ca.CYAES_OK
+            parity = "bit-exact" if all_ok(ok) else "MISMATCH"
+            log("config E parity: %s (golden passes verified on rank %d: %s)" % (parity, rank, verified))
+
+        ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+                torch.cuda.Event(enable_timing=True)) for _ in mine] for _ in range(steps)]
+        t_aes, t_fill = 0.0, 0.0
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_begin = time.perf_counter()
+        for s in range(steps):
+            for j, i in enumerate(mine):
+                f0 = time.perf_counter()
+                fill(i)  # input staging: the pass's payloads arrive in HBM (untimed)
+                torch.cuda.synchronize()
+                a0 = time.perf_counter()
+                ev[s][j][0].record(stream)
+                enc()
+                ev[s][j][1].record(stream)
+                dec()
+                ev[s][j][2].record(stream)
+                torch.cuda.synchronize()
+                a1 = time.perf_counter()
+                t_fill += a0 - f0
+                t_aes += a1 - a0
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t_wall = time.perf_counter() - t_begin
+        t = max_over_ranks(t_aes)
+        shards = None
+        if world > 1:
+            shards = [None] * world
+            dist.all_gather_object(shards, {"rank": rank, "passes": mine, "golden_verified": verified})
+        else:
+            shards = [{"rank": 0, "passes": mine, "golden_verified": verified}]
+        n = steps * len(mine)
+        res = {
+            "name": "E", "npay": pp, "pb": pb, "ppk": 0, "nbytes": nbytes, "t": t, "steps": steps,
+            "value": 2.0 * nbytes * passes * steps / t / gib,
+            "enc_ms": sum(a.elapsed_time(b) for row in ev for a, b, _ in row) / n,
+            "dec_ms": sum(b.elapsed_time(c) for row in ev for _, b, c in row) / n,
+            "parity": parity, "d_ct": d_ct, "d_pt": d_pt, "passes_per_gpu": len(mine), "passes": passes,
+            "fill_ms": max_over_ranks(t_fill) / steps * 1e3, "wall_ms": max_over_ranks(t_wall) / steps * 1e3,
+            "shards": shards,
+        }
+        # leave pass 0's cipher in d_ct for the cpu baseline sample (rank 0 at N=1 walks it)
+        if rank == 0 and world == 1 and mine[0] == 0:
+            fill(0)
+            enc()
+        del d_rt
+        return res
+
+    if args.config == "E":
+        main_res = run_e(args.steps, args.warmup, not args.no_verify)
+    else:
+        main_res = run_config(args.config, args.payloads or CONFIGS[args.config][0], args.steps, args.warmup,
+                              not args.no_verify, keep_cipher=True)
     nbytes, pb, ppk = main_res["nbytes"], main_res["pb"], main_res["ppk"]
     npay, t, value = main_res["npay"], main_res["t"], main_res["value"]
     enc_ms, dec_ms, parity = main_res["enc_ms"], main_res["dec_ms"], main_res["parity"]
 
+    # In-kernel shader clock under this load: the clock-probe build of the same
+    # kernels on the same buffers (s_memtime cycles / s_memrealtime 100 MHz ticks
+    # per wave, tools/clockcal.hip).  Untimed; measurement only.
+    clock = None
+    probe_path = os.path.join(ROOT, "build", "variants", "clockprobe.so")
+    if not args.no_clock and os.path.exists(probe_path) and main_res.get("d_pt") is not None:
+        import ctypes
+        plib = ca.load_library(probe_path)
+        pctx = ca.GpuContext(device, lib=plib)
+        if ppk:
+            pctx.set_keys(session_keys((npay + ppk - 1) // ppk))
+        else:
+            pctx.set_keys(bytes(range(16)))
+        d_tmp = torch.empty_like(main_res["d_ct"])
+        buf = (ctypes.c_ulonglong * 8)()
+        for r in range(4):
+            pctx.encrypt_uniform(main_res["d_pt"], d_tmp, npay, pb, payloads_per_key=ppk, stream=sh)
+            pctx.decrypt_uniform(d_tmp, d_tmp, npay, pb, payloads_per_key=ppk, stream=sh)
+            torch.cuda.synchronize()
+            if r == 0:
+                plib.cyaes_debug_probe(buf)  # first launch: clock ramp; discard
+        plib.cyaes_debug_probe(buf)
+        clock = {k: (buf[4 * i] / buf[4 * i + 1] * 0.1 if buf[4 * i + 1] else None)
+                 for i, k in enumerate(("encrypt", "decrypt"))}
+        pctx.close()
+        del d_tmp
+
     def roof(ms, nb=nbytes):
         ach = 2.0 * nb / (ms / 1e3) / 1e9  # algorithmic: read N + write N per launch
-        return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4)}
+        return {"bound": "lds", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "frac_vs_copy_ceiling": round(ach / HBM_COPY_CEILING_GBS, 4)}
 
-    def lds(ms, nb=nbytes):
-        # The binding on-chip resource: 160 conflict-free ds_read_b32
-        # lookups per 16-B block; nominal LDS rate 32 lanes/clk/CU (2 cycles per wave64
-        # ds_read_b32), here priced at the 2.4 GHz peak shader clock.  In-kernel clock
-        # probes (tools/ab.py + CYAES_CLOCK_PROBE) show ~1.9 GHz under this load.
+    def ceiling(ms, ghz, nb=nbytes):
+        # The binding on-chip resource (DESIGN.md §3.4): 160 conflict-free
+        # ds_read_b32 lookups per 16-B block, issued at 32 lanes/clk/CU.
         look = LOOKUPS_PER_BLOCK * (nb / 16) / (ms / 1e3)
-        peak = LDS_LANES_PER_CLK_CU * NUM_CUS * 2.4e9
-        return {"lookups_per_s": float("%.4g" % look), "peak_at_2p4ghz": float("%.4g" % peak),
-                "frac": round(look / peak, 4)}
+        out = {"unit": "LDS lookups/clk/CU", "lookups_per_s": float("%.4g" % look),
+               "peak_nominal": LDS_LANES_PER_CLK_CU, "peak_microbench": LDS_MEASURED_PEAK,
+               "frac_at_2p4ghz": round(look / (LDS_LANES_PER_CLK_CU * NUM_CUS * 2.4e9), 4)}
+        if ghz:
+            per_clk = look / (NUM_CUS * ghz * 1e9)
+            out.update(clock_ghz=round(ghz, 3), clock_source="in-kernel s_memtime/s_memrealtime, clockprobe.so",
+                       achieved=round(per_clk, 2), frac=round(per_clk / LDS_LANES_PER_CLK_CU, 4))
+        return out
 
-    kern = {"encrypt": dict(roof(enc_ms), avg_ms=round(enc_ms, 4), lds=lds(enc_ms)),
-            "decrypt": dict(roof(dec_ms), avg_ms=round(dec_ms, 4), lds=lds(dec_ms))}
+    kern = {k: dict(roof(ms), avg_ms=round(ms, 4), ceiling=ceiling(ms, (clock or {}).get(k)))
+            for k, ms in (("encrypt", enc_ms), ("decrypt", dec_ms))}
     dom = "encrypt" if enc_ms >= dec_ms else "decrypt"
-    roofline = dict(roof(enc_ms if dom == "encrypt" else dec_ms), kernel=dom, traffic=None)
+    roofline = dict(roof(enc_ms if dom == "encrypt" else dec_ms), kernel=dom, traffic=None,
+                    ceiling=kern[dom]["ceiling"])
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
-        tr = json.load(open(tfile)).get(args.config, {}).get(dom)
+        tr = json.load(open(tfile)).get("C" if args.config == "E" else args.config, {}).get(dom)
         if tr:
             roofline["traffic"] = tr.get("bytes_per_launch")
             roofline["traffic_note"] = tr.get("note")
@@ -272,8 +451,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         log("cpu baseline ...")
-        cpu = cpu_baseline(args.config, npay, pb, ppk, main_res["d_ct"], torch, args.cpu_sample)
-    main_res["d_ct"] = None
+        cpu = cpu_baseline("C (= config E pass 0)" if args.config == "E" else args.config, npay, pb, ppk,
+                           main_res["d_ct"], torch, args.cpu_sample)
+    main_res["d_ct"] = main_res["d_pt"] = None
     torch.cuda.empty_cache()
 
     # The north star's other named packet sizes, at the same GPU count: MTU-sized
@@ -294,20 +474,36 @@ def main():
         torch.cuda.empty_cache()
 
     if rank == 0:
+        if args.config == "E":
+            P = main_res["passes"]
+            workload = ("config E: %d payloads x %d B in total (%.0f GiB), %d fixed passes of %d payloads "
+                        "(%.2f GiB, config C's batch); %d GPU(s) x %d passes each, 1 key RCCL-broadcast, "
+                        "encrypt+decrypt, device-resident, AES-128-CBC chain per payload from DefaultIV"
+                        % (P * npay, pb, P * nbytes / gib, P, npay, nbytes / gib, world, P // world))
+            step_bytes = P * nbytes
+        else:
+            workload = ("config %s: %d payloads x %d B per GPU (%.2f GiB), %s, encrypt+decrypt, device-resident, "
+                        "AES-128-CBC chain per payload from DefaultIV"
+                        % (args.config, npay, pb, nbytes / gib,
+                           ("%d payloads per session key" % ppk) if ppk else "1 key"))
+            step_bytes = nbytes * world
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": "config %s: %d payloads x %d B per GPU (%.2f GiB), %s, encrypt+decrypt, "
-                                   "device-resident, AES-128-CBC chain per payload from DefaultIV"
-                                   % (args.config, npay, pb, nbytes / gib,
-                                      ("%d payloads per session key" % ppk) if ppk else "1 key"),
-                       "payloads_per_gpu": npay, "payload_bytes": pb, "parallelism": "payload shards x%d, "
-                       "RCCL key broadcast" % world},
-            "hbm_frac_step": round(4.0 * nbytes * world / (t / args.steps) / 1e9 / (HBM_PEAK_GBS * world), 4),
+            "scaling": "strong" if args.config == "E" else "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": workload, "payloads_per_pass" if args.config == "E" else "payloads_per_gpu": npay,
+                       "payload_bytes": pb, "parallelism": "payload shards x%d, RCCL key broadcast" % world},
+            "hbm_frac_step": round(4.0 * step_bytes / (t / args.steps) / 1e9 / (HBM_PEAK_GBS * world), 4),
             "roofline": roofline, "kernels": kern, "cpu_baseline": cpu, "parity": parity,
             "packet_configs": packet_configs,
         }
+        if args.config == "E":
+            out["config"].update(passes=main_res["passes"], passes_per_gpu=main_res["passes_per_gpu"])
+            out["timing"] = {"timed": "per pass: encrypt + decrypt between device synchronisations, summed; "
+                                      "max over ranks", "fill_ms_per_step": round(main_res["fill_ms"], 3),
+                             "wall_ms_per_step_incl_fill": round(main_res["wall_ms"], 3)}
+            out["shards"] = main_res["shards"]
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

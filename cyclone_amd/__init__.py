@@ -526,6 +526,15 @@ class Batcher:
                 dst = src if out is inp else _Buf(out, True)
             if size is None:
                 size = src.n
+            # native code copies `size` bytes from/to these buffers: bound it as submit() does
+            if op == OP_RELAY_SEAL:
+                bad = size > src.n or relay_packet_bytes(size) > dst.n
+            else:
+                bad = size > src.n or size > dst.n
+            if bad:
+                for t in tokens:
+                    self._untrack(t)
+                raise ValueError("request %d: size exceeds its buffer" % i)
             token = self._track((src, dst), done)
             tokens.append(token)
             arr[i] = BatchReq(op, slot, conn or 0, src.ptr, dst.ptr, size, self._cb, token)

@@ -62,6 +62,8 @@ struct Req {
     cyaes_done_fn done;
     void* user;
     Clock::time_point t;
+    uint64_t seq;       // 1-based position in its shard's queue (flush watermark)
+    uint8_t shard;
     uint64_t data_bytes() const { return up16(op >= CYAES_OP_RELAY_SEAL ? 16 + crypt : size); }
 };
 
@@ -214,6 +216,13 @@ struct cyaes_batcher {
     std::deque<Stage*> inflight;
     bool builder_done = false;
     uint64_t completed = 0;
+    // Per-shard completion watermark: the highest seq completed.  A shard's
+    // requests complete in enqueue order (the builder appends each shard's
+    // queue to carry in order, cuts batches in carry order, and batches
+    // complete in launch order), so flush waits for every shard's watermark to
+    // reach that shard's count at the call -- a global count could be reached
+    // by later requests of other shards while earlier ones are still queued.
+    std::array<uint64_t, kShards> done_seq{};
     uint64_t batches = 0, bytes = 0, max_batch = 0, errors = 0;
     int first_error = CYAES_OK;
 
@@ -528,8 +537,10 @@ void cyaes_batcher::complete_loop() {
         // relay-shaped load of tools/bench_batcher.cpp: the callbacks then
         // contend with the submitting threads.)
         uint64_t nbytes = 0;
+        std::array<uint64_t, kShards> hi{};
         for (const Req& r : st->reqs) {
             nbytes += r.crypt;
+            hi[r.shard] = std::max(hi[r.shard], r.seq);
             if (r.done) r.done(r.user, status);
         }
         const size_t nreq = st->reqs.size();
@@ -539,6 +550,7 @@ void cyaes_batcher::complete_loop() {
         pc.reqs += (int64_t)nreq;
         lk.lock();
         completed += nreq;
+        for (int i = 0; i < kShards; i++) done_seq[i] = std::max(done_seq[i], hi[i]);
         batches++;
         bytes += nbytes;
         max_batch = std::max<uint64_t>(max_batch, nreq);
@@ -629,6 +641,8 @@ void cyaes_batcher::enqueue(Req* rs, size_t n, uint64_t nbytes) {
         std::lock_guard<std::mutex> lk(sh.mu);
         for (size_t i = 0; i < n; i++) {
             rs[i].t = t;
+            rs[i].seq = sh.enqueued + i + 1;
+            rs[i].shard = (uint8_t)s;
             sh.q.push_back(std::move(rs[i]));
         }
         sh.bytes += nbytes;
@@ -806,11 +820,19 @@ int cyaes_batcher_submit_many(cyaes_batcher* b, const cyaes_batch_req* reqs, uin
 
 int cyaes_batcher_flush(cyaes_batcher* b) {
     if (!b) return CYAES_EINVAL;
-    const uint64_t target = b->enqueued_total();
+    std::array<uint64_t, kShards> target;  // every shard's queue length at the call
+    for (int i = 0; i < kShards; i++) {
+        std::lock_guard<std::mutex> sl(b->shards[i].mu);
+        target[i] = b->shards[i].enqueued;
+    }
     std::unique_lock<std::mutex> lk(b->mu);
     b->flushers.fetch_add(1);
     b->cv_submit.notify_all();
-    b->cv_flush.wait(lk, [&] { return b->completed >= target; });
+    b->cv_flush.wait(lk, [&] {
+        for (int i = 0; i < kShards; i++)
+            if (b->done_seq[i] < target[i]) return false;
+        return true;
+    });
     b->flushers.fetch_sub(1);
     const int err = b->first_error;
     b->first_error = CYAES_OK;

@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <new>
@@ -25,13 +26,11 @@ struct cyaes_gpu {
     uint32_t* d_keys = nullptr;    // nkeys * kSchedWords
     uint32_t nkeys = 0;
     uint32_t key_cap = 0;
-    uint4* d_boundary = nullptr;
-    uint64_t boundary_cap = 0;
-    uint8_t* d_iv_scratch = nullptr;
-    uint64_t iv_cap = 0;
     uint32_t* d_status = nullptr;
     unsigned long long* d_digest = nullptr;
-    hipStream_t last_stream = nullptr;
+    // Stream of the latest batch (cyaes_gpu_check syncs it); batches may be
+    // issued from several threads (drop-in leaders, the batcher).
+    std::atomic<hipStream_t> last_stream{nullptr};
     struct HostPipe* pipe = nullptr;  // cyaes_gpu_{en,de}crypt_host, created on first use
 };
 
@@ -66,16 +65,6 @@ struct DeviceGuard {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-template <typename T>
-int ensure(T** buf, uint64_t* cap, uint64_t want_elems) {
-    if (*cap >= want_elems) return CYAES_OK;
-    if (*buf) CY_TRY(hipFree(*buf));
-    *buf = nullptr;
-    *cap = 0;
-    CY_TRY(hipMalloc(reinterpret_cast<void**>(buf), want_elems * sizeof(T)));
-    *cap = want_elems;
-    return CYAES_OK;
-}
 
 // Validates the key-selection arguments of a batch and fills a KeySel.  The
 // key table is the context's, unless a batch brings its own (table != NULL:
@@ -149,14 +138,30 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     return map_err(launch_encrypt(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
 }
 
+// Per-call device scratch, stream-ordered (hipMallocAsync / hipFreeAsync on
+// the batch's stream): batches of one context on different streams never share
+// a scratch buffer while a kernel still reads it.
+struct StreamScratch {
+    void* p = nullptr;
+    hipStream_t s = nullptr;
+    int get(uint64_t bytes, hipStream_t stream) {
+        s = stream;
+        CY_TRY(hipMallocAsync(&p, bytes, stream));
+        return CYAES_OK;
+    }
+    ~StreamScratch() {
+        if (p) (void)hipFreeAsync(p, s);  // after the kernels queued on s
+    }
+};
+
 // d_iv_in == d_iv_out on a block-parallel decrypt: a payload's last block may
 // be written before its first block reads the IV, so read from a copy.
-int alias_iv(cyaes_gpu* ctx, const uint8_t** iv_in, const uint8_t* iv_out, uint64_t npayloads, hipStream_t stream) {
+int alias_iv(StreamScratch& sc, const uint8_t** iv_in, const uint8_t* iv_out, uint64_t npayloads, hipStream_t stream) {
     if (!*iv_in || *iv_in != iv_out) return CYAES_OK;
-    int st = ensure(&ctx->d_iv_scratch, &ctx->iv_cap, npayloads * 16);
+    int st = sc.get(npayloads * 16, stream);
     if (st) return st;
-    CY_TRY(hipMemcpyAsync(ctx->d_iv_scratch, *iv_in, npayloads * 16, hipMemcpyDeviceToDevice, stream));
-    *iv_in = ctx->d_iv_scratch;
+    CY_TRY(hipMemcpyAsync(sc.p, *iv_in, npayloads * 16, hipMemcpyDeviceToDevice, stream));
+    *iv_in = static_cast<const uint8_t*>(sc.p);
     return CYAES_OK;
 }
 
@@ -176,7 +181,8 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     const uint64_t nwaves = (uint64_t)grid * kWaves;
     uint64_t bpw = (nblocks + nwaves - 1) / nwaves;
     bpw = (bpw + step - 1) / step * step;
-    st = alias_iv(ctx, &iv_in, iv_out, npayloads, stream);
+    StreamScratch iv_copy, boundary;
+    st = alias_iv(iv_copy, &iv_in, iv_out, npayloads, stream);
     if (st) return st;
     a.in = in;
     a.out = out;
@@ -196,10 +202,11 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     const uint64_t sess_blocks = (uint64_t)ppk * bpp;
     if (!key_idx && ppk && sess_blocks % step == 0) a.sess_blocks = sess_blocks;
     if (in == out && nwaves > 1) {
-        st = ensure(&ctx->d_boundary, &ctx->boundary_cap, nwaves);
+        st = boundary.get(nwaves * sizeof(uint4), stream);
         if (st) return st;
-        CY_TRY(launch_boundary_snapshot(in, nblocks, bpw, nwaves, a.bpp, ctx->d_boundary, stream));
-        a.boundary = ctx->d_boundary;
+        uint4* snap = static_cast<uint4*>(boundary.p);
+        CY_TRY(launch_boundary_snapshot(in, nblocks, bpw, nwaves, a.bpp, snap, stream));
+        a.boundary = snap;
     }
     ctx->last_stream = stream;
     return map_err(launch_decrypt_flat(a, grid, stream));
@@ -211,7 +218,8 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     DecArgs a = {};
     int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys, table, table_keys);
     if (st) return st;
-    st = alias_iv(ctx, &iv_in, iv_out, npayloads, stream);
+    StreamScratch iv_copy;
+    st = alias_iv(iv_copy, &iv_in, iv_out, npayloads, stream);
     if (st) return st;
     a.in = in;
     a.out = out;
@@ -317,6 +325,18 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_status), 16);
     if (e == hipSuccess) e = hipMemset(ctx->d_status, 0, 16);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_digest), 16);
+    if (e == hipSuccess) {
+        // Per-call scratch comes from the device's default pool (StreamScratch):
+        // keep up to 64 MiB of it cached across synchronisations.
+        hipMemPool_t pool = nullptr;
+        uint64_t keep = 64ull << 20;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
+            uint64_t cur = 0;
+            if (hipMemPoolGetAttribute(pool, hipMemPoolAttrReleaseThreshold, &cur) == hipSuccess && cur < keep)
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        }
+        (void)hipGetLastError();
+    }
     if (e != hipSuccess) {
         cyaes_gpu_destroy(ctx);
         return map_err(e);
@@ -331,8 +351,6 @@ void cyaes_gpu_destroy(cyaes_gpu* ctx) {
     (void)hipDeviceSynchronize();
     (void)hipFree(ctx->d_tables);
     (void)hipFree(ctx->d_keys);
-    (void)hipFree(ctx->d_boundary);
-    (void)hipFree(ctx->d_iv_scratch);
     (void)hipFree(ctx->d_status);
     (void)hipFree(ctx->d_digest);
     destroy_pipe(ctx->pipe);
@@ -609,20 +627,22 @@ int dropin_init(DropIn& d) {  // under d.mu
     return CYAES_OK;
 }
 
+// Grows geometrically: hipHostFree / hipFree synchronise, so a run of
+// slightly growing calls must not reallocate every time.
 int dropin_reserve(DropInSlot& d, uint64_t host_bytes, uint64_t dev_bytes) {
     if (d.pinned_cap < host_bytes) {
+        const uint64_t cap = std::max<uint64_t>(host_bytes, 2 * d.pinned_cap);
         if (d.pinned) CY_TRY(hipHostFree(d.pinned));
         d.pinned = nullptr;
         d.pinned_cap = 0;
-        const uint64_t cap = std::max<uint64_t>(host_bytes, 2 * d.pinned_cap);
         CY_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.pinned), cap, hipHostMallocDefault));
         d.pinned_cap = cap;
     }
     if (d.d_cap < dev_bytes) {
+        const uint64_t cap = std::max<uint64_t>(dev_bytes, 2 * d.d_cap);
         if (d.d_buf) CY_TRY(hipFree(d.d_buf));
         d.d_buf = nullptr;
         d.d_cap = 0;
-        const uint64_t cap = std::max<uint64_t>(dev_bytes, 2 * d.d_cap);
         CY_TRY(hipMalloc(reinterpret_cast<void**>(&d.d_buf), cap));
         d.d_cap = cap;
     }

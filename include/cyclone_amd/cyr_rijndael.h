@@ -6,10 +6,12 @@
  * The object holds the same 352-byte schedule (m_Ke/m_Kd); encrypt/decrypt
  * run on the MI355X through the C-ABI in <cyaes.h>.
  *
- * Error behaviour mirrors the reference: a size that is not a multiple of 16
- * or a NULL buffer is an assertion failure (cyr_rijndael.cpp:590-591,614-615).
- * In NDEBUG builds the call is skipped instead of overrunning the buffer, and
- * last_status() reports the C-ABI status.
+ * Error behaviour: fail closed.  A size that is not a multiple of 16 or a NULL
+ * buffer (the reference's asserts, cyr_rijndael.cpp:590-591,614-615) and any
+ * device error (no gfx950 GPU, CYAES_DEVICE out of range, out of memory)
+ * abort the process, in NDEBUG builds too: the relay encrypts in place and
+ * never checks a status, so a skipped call would send plaintext.
+ * last_status() reports the C-ABI status of the last (successful) call.
  */
 #pragma once
 

@@ -12,6 +12,7 @@
  * Build & run (writes tests/golden/openssl_vectors.json):
  *   gcc -O2 -pthread tests/golden/gen_openssl_vectors.c -lcrypto -o /tmp/genv
  *   /tmp/genv > tests/golden/openssl_vectors.json
+ *   /tmp/genv e > tests/golden/config_e_passes.json   (config E, per pass)
  *
  * Workload definitions (DESIGN.md §5 / SURVEY.md §8d):
  *   plaintext word w of payload p = splitmix64(0x5EEDC1C1 + (p << 20) + w), LE
@@ -105,7 +106,8 @@ static void* worker(void* arg) {
     return NULL;
 }
 
-static void config_digest(const char* name, uint64_t p0, uint64_t n, uint32_t bytes, uint32_t ppk, int last) {
+static void config_digest_q(const char* name, uint64_t p0, uint64_t n, uint32_t bytes, uint32_t ppk, int last,
+                            int quote) {
     enum { T = 8 };
     pthread_t th[T];
     job jobs[T];
@@ -120,15 +122,45 @@ static void config_digest(const char* name, uint64_t p0, uint64_t n, uint32_t by
         pthread_join(th[t], NULL);
         px ^= jobs[t].px; ps += jobs[t].ps; cx ^= jobs[t].cx; cs += jobs[t].cs;
     }
-    printf("  \"%s\": {\"p0\": %llu, \"npayloads\": %llu, \"payload_bytes\": %u, \"payloads_per_key\": %u, "
+    printf(quote ? "  \"%s\": {\"p0\": %llu," : "  {\"pass\": %s, \"p0\": %llu, \"npayloads\": %llu, \"payload_bytes\": %u, \"payloads_per_key\": %u, "
            "\"plain_digest\": [\"%016llx\", \"%016llx\"], \"cipher_digest\": [\"%016llx\", \"%016llx\"]}%s\n",
            name, (unsigned long long)p0, (unsigned long long)n, bytes, ppk, (unsigned long long)px,
            (unsigned long long)ps, (unsigned long long)cx, (unsigned long long)cs, last ? "" : ",");
     fflush(stdout);
 }
 
-int main(void) {
+static void config_digest(const char* name, uint64_t p0, uint64_t n, uint32_t bytes, uint32_t ppk, int last) {
+    config_digest_q(name, p0, n, bytes, ppk, last, 1);
+}
+
+/* Config E (BASELINE.json configs[4]): 2^23 payloads x 64 KiB in fixed passes
+ * of 2^18 payloads; pass i covers payloads [i*2^18, (i+1)*2^18)
+ * and GPU g of G walks passes [g*32/G, (g+1)*32/G), so these 32 digests cover
+ * every shard at G = 1, 2, 4, 8.  "reduced": the same walk with passes of 4096
+ * payloads (the 2-rank GPU test). */
+static void config_e(void) {
+    char name[16];
+    printf("{\n \"generator\": \"tests/golden/gen_openssl_vectors.c e (OpenSSL %s)\",\n",
+           OpenSSL_version(OPENSSL_VERSION));
+    printf(" \"payload_bytes\": 65536,\n \"reduced\": {\"pass_payloads\": 4096, \"passes\": [\n");
+    for (int i = 0; i < 8; i++) {
+        snprintf(name, sizeof name, "%d", i);
+        config_digest_q(name, 4096ull * i, 4096, 65536, 0, i == 7, 0);
+    }
+    printf(" ]},\n \"full\": {\"pass_payloads\": 262144, \"passes\": [\n");
+    for (int i = 0; i < 32; i++) {
+        snprintf(name, sizeof name, "%d", i);
+        config_digest_q(name, 262144ull * i, 262144, 65536, 0, i == 31, 0);
+    }
+    printf(" ]}\n}\n");
+}
+
+int main(int argc, char** argv) {
     char hb[2 * 65536 + 1];
+    if (argc > 1 && !strcmp(argv[1], "e")) {
+        config_e();
+        return 0;
+    }
     uint8_t a[128], b[128];
     printf("{\n \"generator\": \"tests/golden/gen_openssl_vectors.c (OpenSSL %s)\",\n",
            OpenSSL_version(OPENSSL_VERSION));

@@ -120,3 +120,31 @@ def test_mgpu_without_device_fails_loudly():
     with pytest.raises(ca.CyaesError) as e:
         ca.MultiGpu([0])
     assert e.value.status == ca.CYAES_ENODEV
+
+
+def test_relay_call_expressions_compile():
+    """samples/relay's Rijndael expressions, verbatim (tests/cpp/relay_calls.cpp:
+    relay_local.cpp:204-207,329-334,343,363-366), compile and link against the
+    drop-in header unchanged -- INTEGRATION.md §1's claim, as a build."""
+    subprocess.run(["make", "-C", ROOT, "-s", "cpptest"], check=True)
+    exe = os.path.join(ROOT, "build", "relay_calls")
+    src = open(os.path.join(ROOT, "tests", "cpp", "relay_calls.cpp")).read()
+    for expr in ("pipe->m_encrypt = new Rijndael(pipe->m_secretKey.bytes);",
+                 "for (size_t i = 0; i < Rijndael::BLOCK_SIZE; i++)",
+                 "pipe->m_encrypt->encrypt(buf, buf, buf_round_size);",
+                 "pipe->m_decrypt->decrypt(buf, buf, packet.get_packet_size() - sizeof(RelayForwardMsg));",
+                 "memset(pipe->m_secretKey.bytes, 0, Rijndael::BLOCK_SIZE);"):
+        assert expr in src, expr
+    assert subprocess.run([exe, "--compile"]).returncode == 0
+
+
+def test_dropin_fails_closed():
+    """A drop-in call that cannot run on the GPU aborts (NDEBUG build included)
+    instead of returning with the relay's buffer still plaintext.  Here: a
+    device index that does not exist (and, in this container, no GPU at all)."""
+    subprocess.run(["make", "-C", ROOT, "-s", "cpptest"], check=True)
+    p = subprocess.run([os.path.join(ROOT, "build", "relay_calls")], capture_output=True, text=True,
+                       env=dict(os.environ, CYAES_DEVICE="99"), timeout=120)
+    assert p.returncode == -6, (p.returncode, p.stdout, p.stderr)  # SIGABRT
+    assert "aborting rather than leave the buffer unprocessed" in p.stderr
+    assert "relay_calls: ok" not in p.stdout

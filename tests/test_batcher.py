@@ -205,6 +205,53 @@ def test_large_requests_fill_several_batches():
         b.close()
 
 
+def test_flush_waits_for_own_requests_under_load():
+    """flush() returns only after every request submitted before it completed,
+    while other threads keep submitting into small batches (a global
+    completion count could be reached by later requests of other shards)."""
+    b = ca.Batcher(0, max_batch_bytes=64 << 10, max_delay_us=20, inflight=3)
+    try:
+        key = _keys(1, 11)[0]
+        s = b.session_open(key)
+        stop = threading.Event()
+
+        def noise(t):
+            rng = random.Random(t)
+            while not stop.is_set():
+                n = 16 * rng.randrange(1, 1024)
+                b.submit(ca.OP_ENCRYPT, s, bytes(n), bytearray(n))
+
+        th = [threading.Thread(target=noise, args=(t,)) for t in range(6)]
+        for t in th:
+            t.start()
+        try:
+            for rnd in range(20):
+                done = []
+                for i in range(40):
+                    n = 16 * (1 + (i * 37 + rnd) % 2000)
+                    b.submit(ca.OP_DECRYPT, s, bytes(n), bytearray(n), None, lambda st, i=i: done.append(i))
+                assert b.flush() == ca.CYAES_OK
+                assert sorted(done) == list(range(40)), (rnd, len(done))
+        finally:
+            stop.set()
+            for t in th:
+                t.join()
+        assert b.flush() == ca.CYAES_OK and b.stats()["pending"] == 0
+    finally:
+        b.close()
+
+
+def test_submit_many_rejects_oversized_requests(batcher):
+    s = batcher.session_open(_keys(1, 12)[0])
+    with pytest.raises(ValueError):
+        batcher.submit_many([(ca.OP_ENCRYPT, s, bytes(32), bytearray(16), 32, None, 0)])
+    with pytest.raises(ValueError):
+        batcher.submit_many([(ca.OP_DECRYPT, s, bytes(16), bytearray(64), 64, None, 0)])
+    with pytest.raises(ValueError):
+        batcher.submit_many([(ca.OP_RELAY_SEAL, s, bytes(100), bytearray(64), None, None, 1)])
+    batcher.session_close(s)
+
+
 def test_device_relay_stream_in_place():
     """A connection's byte stream of relay packets, resident in HBM: the
     payloads (packet offset 12, 4-byte aligned) are encrypted and decrypted

@@ -1,0 +1,90 @@
+"""Config E (BASELINE.json configs[4]): 8 M x 64 KiB payloads in 32 fixed passes
+of 2^18, GPU g of G walking passes [g*32/G, (g+1)*32/G).
+
+CPU: the committed per-pass OpenSSL digests (tests/golden/config_e_passes.json,
+made by gen_openssl_vectors.c e) agree with the config goldens and with the
+oracle, and the pass split covers the job at G = 1, 2, 4, 8.
+GPU: bench.py's multi-rank path -- key broadcast, pass shards, per-rank
+parity against the pass digests -- run as a fresh 2-rank torchrun child
+process on the box's one GPU (gloo; ranks share the device).  Every relay
+payload is its own chain from DefaultIV (relay_local.cpp:206,
+relay_server.cpp:472), so shards are independent."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def _e():
+    return json.load(open(os.path.join(GOLDEN, "config_e_passes.json")))
+
+
+def test_pass_digests_consistent_with_config_goldens():
+    e = _e()
+    cfg = json.load(open(os.path.join(GOLDEN, "openssl_vectors.json")))["configs"]
+    full = e["full"]["passes"]
+    assert e["payload_bytes"] == 65536 and e["full"]["pass_payloads"] == 262144 and len(full) == 32
+    assert 32 * 262144 == 1 << 23  # 8 M payloads in total
+    for i, g in enumerate(full):
+        assert g["pass"] == i and g["p0"] == i * 262144 and g["npayloads"] == 262144
+    # pass 0 is config C's batch, pass 1 the old rank-1 shard
+    for k in ("plain_digest", "cipher_digest"):
+        assert full[0][k] == cfg["C"][k]
+        assert full[1][k] == cfg["E_rank1"][k]
+    assert len({tuple(g["cipher_digest"]) for g in full}) == 32
+
+
+@pytest.mark.parametrize("gpus", [1, 2, 4, 8])
+def test_pass_split_covers_job(gpus):
+    passes = 32
+    walked = []
+    for r in range(gpus):
+        mine = list(range(r * passes // gpus, (r + 1) * passes // gpus))
+        assert len(mine) == passes // gpus
+        walked += mine
+    assert walked == list(range(passes))
+
+
+def test_reduced_pass_digest_matches_oracle():
+    import oracle
+    e = _e()["reduced"]
+    g = e["passes"][5]
+    pp = e["pass_payloads"]
+    pt = oracle.synthetic(5 * pp, pp, 65536)
+    ct = oracle.batch(False, [bytes(range(16))], 0, pt, 65536, nthreads=8)
+    assert ["%016x" % v for v in oracle.digest(pt)] == g["plain_digest"]
+    assert ["%016x" % v for v in oracle.digest(ct)] == g["cipher_digest"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.gpu
+def test_two_rank_config_e_bit_exact(tmp_path):
+    """bench.py --config E on 2 ranks (torchrun child process; gloo, one device)."""
+    env = dict(os.environ, CYAES_BENCH_SAME_DEVICE="1", CYAES_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "E", "--e-pass-payloads", "4096",
+           "--e-passes", "8", "--steps", "2", "--warmup", "1", "--packet-configs", "none", "--no-cpu", "--no-clock"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    (tmp_path / "stderr.txt").write_text(p.stderr)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["parity"] == "bit-exact"
+    assert out["n_gpus"] == 2 and out["config"]["passes"] == 8 and out["config"]["passes_per_gpu"] == 4
+    shards = sorted(out["shards"], key=lambda s: s["rank"])
+    assert [s["passes"] for s in shards] == [[0, 1, 2, 3], [4, 5, 6, 7]]
+    # every pass of every rank matched its committed OpenSSL pass digest
+    assert [s["golden_verified"] for s in shards] == [[0, 1, 2, 3], [4, 5, 6, 7]]
+    assert out["value"] > 0 and out["roofline"]["bound"] == "lds"

@@ -91,6 +91,15 @@ def test_reference_testcase_cpp(torch):
     assert "All tests passed" in r.stdout
 
 
+def test_relay_call_expressions_run(torch):
+    """relay_local.cpp's Rijndael expressions, verbatim, run on the GPU (in-place
+    encrypt of a 0xCE-padded chunk, in-place decrypt of packet_size - 8 bytes)."""
+    subprocess.run(["make", "-C", ROOT, "-s", "cpptest"], check=True)
+    r = subprocess.run([os.path.join(ROOT, "build", "relay_calls")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "relay_calls: ok" in r.stdout
+
+
 def test_dropin_python_kat_stream_inplace(golden):
     k = golden["kat"]
     aes = ca.Rijndael(bytes.fromhex(k["key"]))
@@ -200,6 +209,31 @@ def test_in_place_batches(torch, ctx):
     assert np.array_equal(host(d), want)
     ctx.decrypt_uniform(d, d, n, pb)
     assert np.array_equal(host(d), pt)
+
+
+def test_in_place_decrypts_on_two_streams(torch, ctx):
+    """Two in-place decrypts (boundary snapshots) and two aliased-IV decrypts of
+    one context on two streams at once: each call's scratch is its own."""
+    pb, n = 1472, 40000
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    pts = [oracle.synthetic(7 + 100000 * i, n, pb) for i in range(2)]
+    cts = [oracle.batch(False, [K0], 0, pt, pb, nthreads=16) for pt in pts]
+    ds = [dev(torch, ct) for ct in cts]
+    ivs = [dev(torch, np.tile(np.frombuffer(bytes(range(16)), np.uint8), n)) for _ in range(2)]
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for i, s in enumerate((s1, s2)):
+            ctx.decrypt_uniform(ds[i], ds[i], n, pb, stream=s.cuda_stream)
+        for i, s in enumerate((s1, s2)):
+            ctx.encrypt_uniform(ds[i], ds[i], n, pb, stream=s.cuda_stream)
+        torch.cuda.synchronize()
+    for i, s in enumerate((s1, s2)):  # aliased IV in/out: a per-call copy of the IVs
+        ctx.decrypt_uniform(ds[i], ds[i], n, pb, iv_in=ivs[i], iv_out=ivs[i], stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert np.array_equal(host(ds[i]), pts[i])
+        assert np.array_equal(host(ivs[i]).reshape(n, 16), cts[i].reshape(n, pb // 16, 16)[:, -1])
+    assert ctx.check() == ca.CYAES_OK
 
 
 def test_session_keys_payloads_per_key(torch, ctx):
