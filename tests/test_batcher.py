@@ -216,10 +216,14 @@ def test_flush_waits_for_own_requests_under_load():
         stop = threading.Event()
 
         def noise(t):
+            # a relay-style window: at most 32 requests of this thread in flight
             rng = random.Random(t)
+            window = threading.Semaphore(32)
             while not stop.is_set():
+                if not window.acquire(timeout=0.5):
+                    continue
                 n = 16 * rng.randrange(1, 1024)
-                b.submit(ca.OP_ENCRYPT, s, bytes(n), bytearray(n))
+                b.submit(ca.OP_ENCRYPT, s, bytes(n), bytearray(n), None, lambda st, w=window: w.release())
 
         th = [threading.Thread(target=noise, args=(t,)) for t in range(6)]
         for t in th:

@@ -76,7 +76,7 @@ def test_two_rank_config_e_bit_exact(tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "E", "--e-pass-payloads", "4096",
            "--e-passes", "8", "--steps", "2", "--warmup", "1", "--packet-configs", "none", "--no-cpu", "--no-clock"]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=130)
     (tmp_path / "stderr.txt").write_text(p.stderr)
     assert p.returncode == 0, p.stderr[-4000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]

@@ -86,7 +86,7 @@ def test_reference_testcase_cpp(torch):
     """The C++ re-expression of cyt_unit_crypt.cpp:173-248 against the drop-in class."""
     subprocess.run(["make", "-C", ROOT, "-s", "cpptest"], check=True)
     r = subprocess.run([os.path.join(ROOT, "build", "test_rijndael"), os.path.join(ROOT, "tests/golden/ref_kat.txt")],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "All tests passed" in r.stdout
 
