@@ -30,7 +30,7 @@ AOBJ     := $(BUILD)/cyaes_adler.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
 .PHONY: all lib mgpu oracle cpptest probe microbench variant clean
-all: lib mgpu oracle cpptest probe $(BUILD)/bench_batcher $(BUILD)/dropin_threads
+all: lib mgpu oracle cpptest probe $(BUILD)/bench_batcher $(BUILD)/dropin_threads $(BUILD)/bitslice
 lib: $(LIB)
 mgpu: $(MGPU)
 oracle: $(ORACLE)
@@ -81,6 +81,10 @@ $(PROBE): $(KSRC) $(HDRS) $(HOBJ) $(AOBJ)
 	mkdir -p $(BUILD)/variants
 	$(HIPCC) $(HIPFLAGS) -DCYAES_CLOCK_PROBE=1 -c $(KSRC) -o $(BUILD)/variants/clockprobe.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(BUILD)/variants/clockprobe.o $(AOBJ) $(HOBJ)
+
+# Bitsliced decrypt prototype (measurement tool)
+$(BUILD)/bitslice: tools/bitslice.hip tools/bitslice_gen.h $(LIB) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
 
 # A/B variants: make variant NAME=x DEFS="-DFOO=1" -> build/variants/x.so
 variant: $(HOBJ) $(AOBJ) | $(BUILD)
