@@ -477,9 +477,10 @@ def main():
         if args.config == "E":
             P = main_res["passes"]
             workload = ("config E: %d payloads x %d B in total (%.0f GiB), %d fixed passes of %d payloads "
-                        "(%.2f GiB, config C's batch); %d GPU(s) x %d passes each, 1 key RCCL-broadcast, "
+                        "(%.2f GiB%s); %d GPU(s) x %d passes each, 1 key RCCL-broadcast, "
                         "encrypt+decrypt, device-resident, AES-128-CBC chain per payload from DefaultIV"
-                        % (P * npay, pb, P * nbytes / gib, P, npay, nbytes / gib, world, P // world))
+                        % (P * npay, pb, P * nbytes / gib, P, npay, nbytes / gib,
+                           ", config C's batch" if npay == E_PASS_PAYLOADS else ", reduced", world, P // world))
             step_bytes = P * nbytes
         else:
             workload = ("config %s: %d payloads x %d B per GPU (%.2f GiB), %s, encrypt+decrypt, device-resident, "

@@ -336,13 +336,27 @@ __device__ __forceinline__ uint4 ldu(const uint8_t* p) {
 }
 __device__ __forceinline__ void stu(uint8_t* p, uint4 v) { *reinterpret_cast<Blk4*>(p) = Blk4{v.x, v.y, v.z, v.w}; }
 // Block i of a payload: 16-B aligned (U = false) or 4-B aligned (U = true).
+// (Measured on a stream of 1 M relay packets, lane kernel, profiles/r02/ab_ragged_stores.txt:
+// 16-B stores at 4-B aligned addresses cost ~0.3 ms of 1.75; the loads ~0.02.
+// Four dword stores instead: 2.54 ms; rotating each step's words into aligned
+// 16-B slots: 2.03 ms (the rotation's registers spill).  The cost probes below
+// stay for A/B builds.)
 template <bool U>
 __device__ __forceinline__ uint4 ldb(const uint8_t* base, uint32_t i) {
+#if CYAES_PROBE_ALIGNED_LOADS  // cost probe only (wrong output): ragged loads from the 16-B aligned address
+    if (U) return *reinterpret_cast<const uint4*>((uintptr_t)(base + 16ull * i) & ~(uintptr_t)15);
+#endif
     if (U) return ldu(base + 16ull * i);
     return reinterpret_cast<const uint4*>(base)[i];
 }
 template <bool U>
 __device__ __forceinline__ void stb(uint8_t* base, uint32_t i, uint4 v) {
+#if CYAES_PROBE_ALIGNED_STORES  // cost probe only (wrong output): ragged stores to the 16-B aligned address
+    if (U) {
+        *reinterpret_cast<uint4*>((uintptr_t)(base + 16ull * i) & ~(uintptr_t)15) = v;
+        return;
+    }
+#endif
     if (U) stu(base + 16ull * i, v);
     else reinterpret_cast<uint4*>(base)[i] = v;
 }
@@ -529,6 +543,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_quad(EncArgs a) {
     if (threadIdx.x == 0) lead = 0;
     uint32_t prog = 0;
     __syncthreads();
+    CLOCK_PROBE(0);
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t q = threadIdx.x & 3u;
     const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
