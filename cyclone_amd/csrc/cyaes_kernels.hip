@@ -40,6 +40,9 @@
 #ifndef CYAES_NO_PREFETCH
 #define CYAES_NO_PREFETCH 0    // A/B only: load each encrypt chunk at its top instead of one chunk ahead
 #endif
+#ifndef CYAES_RAGGED_REGULAR
+#define CYAES_RAGGED_REGULAR 1  // ragged decrypt: strided equal-size payload groups walk positions per lane
+#endif
 #ifndef CYAES_TAIL_PREFETCH
 #define CYAES_TAIL_PREFETCH 1  // encrypt: prefetch a payload's partial last chunk with the chunk before
 #endif
@@ -933,15 +936,29 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         if (holder && nbh == 0 && a.iv_out)  // empty chain: the IV comes back unchanged
             *reinterpret_cast<uint4*>(a.iv_out + 16 * ph) =
                 a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * ph) : default_iv();
+        // Regular group: every payload has nb0 >= 64 blocks and the offsets are
+        // equally strided (a relay stream of MTU-sized packets: payload p at
+        // o + p * packet size).  Then each lane walks its own (payload, block)
+        // position -- +64 blocks a row, at most one payload boundary -- with no
+        // per-row ballots, scalar reads or search (profiles/r02/ab_ragged_regular.txt).
+        const uint32_t nb0 = __builtin_amdgcn_readfirstlane(nbh);  // lane 0 holds a payload
+        const uint64_t off0 = rlane64(offh, 0);
+        const uint64_t ostr = gn > 1 ? rlane64(offh, 1) - off0 : 0;
+        const bool regular = CYAES_RAGGED_REGULAR && nb0 >= 64 &&
+                             __ballot(holder && (nbh != nb0 || offh != off0 + (uint64_t)lane * ostr)) == 0;
+        uint32_t jt = 0, rt = lane - 64u;  // regular: this lane's payload and block; the first row adds 64
         // Inclusive prefix of the group's block counts (64-bit: payloads may be up to 2^28 blocks).
         uint64_t incl = nbh;
+        if (!regular) {
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t t = (uint64_t)__shfl_up((unsigned int)(incl >> 32), d) << 32 | __shfl_up((unsigned int)incl, d);
-            if (lane >= (uint32_t)d) incl += t;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t t = (uint64_t)__shfl_up((unsigned int)(incl >> 32), d) << 32 |
+                                   __shfl_up((unsigned int)incl, d);
+                if (lane >= (uint32_t)d) incl += t;
+            }
         }
         const uint64_t bsh = incl - nbh;  // first flat block of payload `lane`
-        const uint64_t total = rlane64(incl, 63);  // lanes >= gn add 0
+        const uint64_t total = regular ? (uint64_t)gn * nb0 : rlane64(incl, 63);  // lanes >= gn add 0
         uint4 carry = make_uint4(0, 0, 0, 0);
         for (uint64_t base = 0; base < total; base += 64 * R) {
             prio_feedback(leadp, ++prog, kDecPrioDiv);
@@ -951,6 +968,16 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
             bool valid[R];
 #pragma unroll
             for (int k = 0; k < R; k++) {
+                if (regular) {
+                    rt += 64;
+                    if (rt >= nb0) rt -= nb0, jt++;
+                    valid[k] = jt < gn;
+                    rr[k] = rt;
+                    jr[k] = jt;
+                    orow[k] = off0 + (uint64_t)jt * ostr + 16ull * rt;
+                    c[k] = valid[k] ? ldu(a.in + orow[k]) : make_uint4(0, 0, 0, 0);
+                    continue;
+                }
                 const uint64_t rlo = base + 64 * k;
                 const uint64_t g = rlo + lane;
                 valid[k] = g < total;
@@ -996,7 +1023,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                 if (valid[k] && rr[k] == 0)
                     pv[k] = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
                 if (a.iv_out) {  // (uniform branch: every lane runs the bpermute; one from an inactive lane reads 0)
-                    const uint32_t nbj = bperm(nbh, jr[k]);
+                    const uint32_t nbj = regular ? nb0 : bperm(nbh, jr[k]);
                     if (valid[k] && rr[k] + 1 == nbj) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
                 }
             }
