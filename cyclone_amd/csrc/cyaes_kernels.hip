@@ -40,6 +40,9 @@
 #ifndef CYAES_NO_PREFETCH
 #define CYAES_NO_PREFETCH 0    // A/B only: load each encrypt chunk at its top instead of one chunk ahead
 #endif
+#ifndef CYAES_QUAD_DPP_XOR
+#define CYAES_QUAD_DPP_XOR 0
+#endif
 #ifndef CYAES_RAGGED_REGULAR
 #define CYAES_RAGGED_REGULAR 1  // ragged decrypt: strided equal-size payload groups walk positions per lane
 #endif
@@ -517,7 +520,7 @@ constexpr uint32_t kQuadFrom2 = 0x4E;  // [2,3,0,1]
 constexpr uint32_t kQuadFrom3 = 0x93;  // [3,0,1,2]
 template <uint32_t CTRL>
 __device__ __forceinline__ uint32_t qperm(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, CYAES_QUAD_DPP_XOR ? true : false);
 }
 
 // One AES block on a quad: s = word q of (plaintext ^ chain ^ k0) in, word q of the ciphertext out.
@@ -528,7 +531,12 @@ __device__ __forceinline__ uint32_t enc_block_quad(const char* lds, uint32_t lo,
         const uint32_t a1 = ld(lds, addr1(s, lo));                          // T2[b1(s_q)] -> column q-1
         const uint32_t a2 = ld(lds + kHalfB, addr(s, lo, kSel2));           // T3[b2(s_q)] -> column q-2
         const uint32_t a3 = ld(lds + kHalfB, addr(s, lo, region1(kSel3)));  // T4[b3(s_q)] -> column q-3
+#if CYAES_QUAD_DPP_XOR
+        // two-input XORs, so the DPP moves can fold into v_xor_b32's source (VOP2 DPP)
+        s = a0 ^ (qperm<kQuadFrom1>(a1) ^ (qperm<kQuadFrom2>(a2) ^ (qperm<kQuadFrom3>(a3) ^ k[r])));
+#else
         s = xor3(a0, qperm<kQuadFrom1>(a1), xor3(qperm<kQuadFrom2>(a2), qperm<kQuadFrom3>(a3), k[r]));
+#endif
     }
     const uint32_t l0 = ld(lds + kHalfB, addr(s, lo, kSel0));   // S in byte 0 (TL3)
     const uint32_t l1 = ld(lds + kHalfB, addr1(s, lo));         // byte 1 (TL4)
