@@ -983,7 +983,6 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                     rr[k] = rt;
                     jr[k] = jt;
                     orow[k] = off0 + (uint64_t)jt * ostr + 16ull * rt;
-                    c[k] = valid[k] ? ldu(a.in + orow[k]) : make_uint4(0, 0, 0, 0);
                     continue;
                 }
                 const uint64_t rlo = base + 64 * k;
@@ -1019,8 +1018,14 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                     orow[k] = bperm64(offh, j) + 16ull * rr[k];
                 }
                 jr[k] = j;
-                c[k] = valid[k] ? ldu(a.in + orow[k]) : make_uint4(0, 0, 0, 0);
             }
+            // All four rows' loads back to back, unconditionally: a lane past the
+            // group's end loads row 0 lane 0's block (always valid) and its result
+            // is never used (a valid lane's predecessor is valid).  A load under
+            // `valid ? load : 0` joined the branches with a vmcnt(0) wait per row.
+            const uint64_t safe = rlane64(orow[0], 0);
+#pragma unroll
+            for (int k = 0; k < R; k++) c[k] = ldu(a.in + (valid[k] ? orow[k] : safe));
             pv[0] = shr1(c[0], carry);
 #pragma unroll
             for (int k = 1; k < R; k++)
