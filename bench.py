@@ -245,14 +245,22 @@ def main():
         torch.cuda.synchronize()
 
         parity = None
+        shard = {"rank": rank, "p0": p0, "npayloads": npay}
         if verify:
             ok = ctx.digest(d_rt, nbytes, sh) == ctx.digest(d_pt, nbytes, sh)
             g = golden.get(name) if rank == 0 else None
             if g and g["npayloads"] == npay and g["payload_bytes"] == pb and g["p0"] == p0:
                 ok = ok and digests_match(g, d_pt, d_ct, nbytes)
+                shard["golden_verified"] = True
             ok = ok and ctx.check() == ca.CYAES_OK
             parity = "bit-exact" if all_ok(ok) else "MISMATCH"
+            # this rank's cipher digest, for checks of shards no golden covers (tests/test_config_e.py)
+            shard["cipher_digest"] = ["%016x" % v for v in ctx.digest(d_ct, nbytes, sh)]
             log("config %s parity: %s" % (name, parity))
+        shards = [shard]
+        if world > 1:
+            shards = [None] * world
+            dist.all_gather_object(shards, shard)
 
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
                torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
@@ -277,6 +285,7 @@ def main():
             "enc_ms": sum(a.elapsed_time(b) for a, b, _ in ev) / steps,
             "dec_ms": sum(b.elapsed_time(c) for _, b, c in ev) / steps,
             "parity": parity, "d_ct": d_ct if keep_cipher else None, "d_pt": d_pt if keep_cipher else None,
+            "shards": shards,
         }
         del d_rt
         if not keep_cipher:
@@ -469,7 +478,7 @@ def main():
             "steps": r["steps"], "warmup": args.packet_warmup, "payloads_per_gpu": r["npay"], "payload_bytes": r["pb"],
             "payloads_per_key": r["ppk"], "encrypt_ms": round(r["enc_ms"], 4), "decrypt_ms": round(r["dec_ms"], 4),
             "hbm_frac_step": round(4.0 * r["nbytes"] / (r["t"] / r["steps"]) / 1e9 / HBM_PEAK_GBS, 4),
-            "parity": r["parity"],
+            "parity": r["parity"], "shards": r["shards"],
         }
         torch.cuda.empty_cache()
 
@@ -499,12 +508,12 @@ def main():
             "roofline": roofline, "kernels": kern, "cpu_baseline": cpu, "parity": parity,
             "packet_configs": packet_configs,
         }
+        out["shards"] = main_res["shards"]
         if args.config == "E":
             out["config"].update(passes=main_res["passes"], passes_per_gpu=main_res["passes_per_gpu"])
             out["timing"] = {"timed": "per pass: encrypt + decrypt between device synchronisations, summed; "
                                       "max over ranks", "fill_ms_per_step": round(main_res["fill_ms"], 3),
                              "wall_ms_per_step_incl_fill": round(main_res["wall_ms"], 3)}
-            out["shards"] = main_res["shards"]
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -88,3 +88,30 @@ def test_two_rank_config_e_bit_exact(tmp_path):
     # every pass of every rank matched its committed OpenSSL pass digest
     assert [s["golden_verified"] for s in shards] == [[0, 1, 2, 3], [4, 5, 6, 7]]
     assert out["value"] > 0 and out["roofline"]["bound"] == "lds"
+
+
+@pytest.mark.gpu
+def test_two_rank_session_keys_bit_exact():
+    """bench.py --config D on 2 ranks (per-session keys): rank 0 broadcasts the
+    session keys, each rank expands the sessions of its payload range
+    (relay_server.cpp:218-240 key hand-off), and each rank's ciphertext digest
+    equals the oracle's on that shard."""
+    import oracle
+    import bench
+    per_rank, pb, ppk = 2048, 1472, 256
+    env = dict(os.environ, CYAES_BENCH_SAME_DEVICE="1", CYAES_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "D", "--payloads", str(per_rank),
+           "--steps", "2", "--warmup", "1", "--packet-configs", "none", "--no-cpu", "--no-clock"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=130)
+    assert p.returncode == 0, p.stderr[-4000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["parity"] == "bit-exact" and out["n_gpus"] == 2
+    keys = bench.session_keys(2 * per_rank // ppk)
+    for sh in sorted(out["shards"], key=lambda s: s["rank"]):
+        p0, n = sh["p0"], sh["npayloads"]
+        assert (p0, n) == (sh["rank"] * per_rank, per_rank)
+        mine = [keys[16 * k:16 * k + 16] for k in range(p0 // ppk, (p0 + n) // ppk)]
+        ct = oracle.batch(False, mine, ppk, oracle.synthetic(p0, n, pb), pb, nthreads=8)
+        assert ["%016x" % v for v in oracle.digest(ct)] == sh["cipher_digest"], sh["rank"]
