@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""tools/ab_relay_layout.py -- where ragged encrypt loses time on relay streams.
+
+Times cyaes_gpu_encrypt_ragged on N equal payloads under layouts that differ in
+one property at a time: packet stride (payload + header bytes), payload offset
+inside the packet (12 = relay, 16 = 16-B aligned) and in place vs a separate
+output stream.  usage: python tools/ab_relay_layout.py [--n 1048576] [--pb 1472]"""
+import argparse
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1048576)
+    ap.add_argument("--pb", type=int, default=1472)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--lib", default=None)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import cyclone_amd as ca
+    c = ca.GpuContext(0, lib=ca.load_library(os.path.abspath(args.lib)) if args.lib else None)
+    c.set_keys(bytes(range(16)))
+    s = torch.cuda.current_stream()
+    n, pb = args.n, args.pb
+    pt = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
+    c.fill_synthetic(pt, 0, n, pb, 0x5EEDC1C1)
+    ref = torch.empty_like(pt)
+    c.encrypt_uniform(pt, ref, n, pb, stream=s.cuda_stream)
+    nb = torch.full((n,), pb, dtype=torch.int32, device="cuda")
+    # (label, header bytes before the payload, packet stride, in place)
+    layouts = [("contig_out", 0, pb, False), ("contig_inplace", 0, pb, True),
+               ("hdr16_out", 16, pb + 16, False), ("hdr16_inplace", 16, pb + 16, True),
+               ("hdr12_s1488_out", 12, pb + 16, False), ("hdr12_s1488_inplace", 12, pb + 16, True),
+               ("relay_out", 12, pb + 12, False), ("relay_inplace", 12, pb + 12, True)]
+    for label, hdr, stride, inplace in layouts:
+        src = torch.zeros(n * stride + 16, dtype=torch.uint8, device="cuda")
+        src[: n * stride].view(n, stride)[:, hdr:hdr + pb] = pt.view(n, pb)
+        dst = src if inplace else torch.zeros_like(src)
+        off = torch.from_numpy(np.arange(n, dtype=np.uint64) * stride + hdr).to("cuda")
+        ts = []
+        for r in range(args.rounds + 1):
+            if inplace:
+                src[: n * stride].view(n, stride)[:, hdr:hdr + pb] = pt.view(n, pb)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            c.encrypt_ragged(src, dst, off, nb, n, stream=s.cuda_stream)
+            e1.record(s)
+            torch.cuda.synchronize()
+            if r:
+                ts.append(e0.elapsed_time(e1))
+        ok = torch.equal(dst[: n * stride].view(n, stride)[:, hdr:hdr + pb].reshape(-1), ref)
+        print("%-22s %8d x %5d B stride %5d: enc %.4f ms (min %.4f)  %s" %
+              (label, n, pb, stride, statistics.median(ts), min(ts), "ok" if ok else "MISMATCH"), flush=True)
+        del src, dst
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
