@@ -5,8 +5,12 @@ Only tests/ import it, as the checker for include/cyaes_relay.h and the
 batcher's SEAL / OPEN requests.
 
 Parity is pinned by this restatement of the reference code (cited line by
-line) and by the AES oracle's own pins; the reference ships no relay test
-vectors, so the packet layout itself is "restated, not vector-pinned".
+line), by the AES oracle's own pins, and -- for the Packet framing -- by the
+reference's own Packet TEST_CASE (test/unit/cyt_unit_packet.cpp:39-142),
+re-expressed in tests/test_relay.py::test_reference_packet_test_case against
+build_packet / take_packet below.  The reference ships no relay byte vectors,
+so the RELAY_FORWARD layout on top of the framing is restated, not
+vector-pinned.
 """
 import struct
 
@@ -24,14 +28,33 @@ def round16(size):
     return size if (size & 0xF) == 0 else (size & ~0xF) + 0x10
 
 
-def build_packet(head_size, packet_id, content):
-    """Packet::build_from_memory (cye_packet.cpp:107-138) with one content part:
-    0xCE-filled memory (:102), BE u16 size and id (:123-124), content copy."""
-    mem = bytearray([FILL]) * (head_size + len(content))
-    mem[0:2] = struct.pack(">H", len(content))
+def build_packet(head_size, packet_id, content, content2=b""):
+    """Packet::build_from_memory (cye_packet.cpp:107-138): 0xCE-filled memory
+    of head_size + size bytes (:90-105), BE u16 size and id (:123-124), the
+    two content parts copied back to back (:129-137).  A total above 0xFFFF
+    builds nothing (:117-118): None."""
+    assert head_size >= 4  # _resize's assert, cye_packet.cpp:92
+    size = len(content) + len(content2)
+    if size > 0xFFFF:
+        return None
+    mem = bytearray([FILL]) * (head_size + size)
+    mem[0:2] = struct.pack(">H", size)
     mem[2:4] = struct.pack(">H", packet_id)
-    mem[head_size:head_size + len(content)] = content
+    mem[head_size:head_size + size] = bytes(content) + bytes(content2)
     return mem
+
+
+def take_packet(buf, head_size):
+    """Packet::build_from_ringbuf (cye_packet.cpp:166-181) on the bytes buf
+    holds: None while fewer than 2 bytes (the size) or fewer than head_size +
+    size bytes are present, else the packet's memory (head_size + size bytes,
+    the head's reserved bytes included as received)."""
+    if len(buf) < 2:
+        return None
+    size, = struct.unpack(">H", bytes(buf[0:2]))
+    if len(buf) < head_size + size:
+        return None
+    return bytes(buf[:head_size + size])
 
 
 def seal_forward(key, conn_id, chunk, encrypt=True):
@@ -68,14 +91,16 @@ def open_forward(key, pkt):
     return conn_id, bytes(pkt[12:12 + size]), bytes(pkt)
 
 
-def parse_stream(stream):
-    """Packet::build_from_ringbuf in a loop (cye_packet.cpp:166-181): a packet
-    is taken when head_size + packet_size bytes are present."""
+def parse_stream(stream, head_size=RELAY_PACKET_HEADSIZE):
+    """take_packet (Packet::build_from_ringbuf, cye_packet.cpp:166-181) in a
+    loop, as the relay's onMessage handlers drain a connection's ring buffer:
+    returns [(offset, packet_size, packet_id)] and the bytes consumed."""
     out, pos = [], 0
-    while len(stream) - pos >= RELAY_PACKET_HEADSIZE:
-        psize, pid = struct.unpack(">HH", stream[pos:pos + 4])
-        if len(stream) - pos < RELAY_PACKET_HEADSIZE + psize:
+    while True:
+        mem = take_packet(stream[pos:], head_size)
+        if mem is None:
             break
+        psize, pid = struct.unpack(">HH", mem[0:4])
         out.append((pos, psize, pid))
-        pos += RELAY_PACKET_HEADSIZE + psize
+        pos += len(mem)
     return out, pos

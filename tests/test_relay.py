@@ -32,6 +32,64 @@ def test_build_forward_matches_reference_packet(size):
     assert struct.unpack(">HH", pkt[:4]) == (8 + ro.round16(size), ro.RELAY_FORWARD)
 
 
+def _check_packet(mem, size, pid, head_size, content):
+    """PACKET_CHECK (cyt_unit_packet.cpp:18-23): BE u16 size and id in the
+    first 4 bytes, memory size = head + packet size, content."""
+    assert mem is not None
+    assert bytes(mem[0:4]) == struct.pack(">HH", size, pid)
+    assert len(mem) == head_size + size
+    assert struct.unpack(">H", bytes(mem[2:4]))[0] == pid and struct.unpack(">H", bytes(mem[0:2]))[0] == size
+    assert bytes(mem[head_size:head_size + size]) == bytes(content[:size])
+
+
+def test_reference_packet_test_case():
+    """The reference's own Packet TEST_CASE (test/unit/cyt_unit_packet.cpp:39-142),
+    re-expressed against the framing restatement (relay_oracle.build_packet /
+    take_packet) and, at the relay's head size of 4, against cyaes_relay_parse.
+    The test's rand() bytes become a seeded generator; build_from_pipe
+    (:108-121) is not restated: the relay reads connections through ring
+    buffers (Packet::build_from_ringbuf), which is what the product parses."""
+    HEAD_SIZE, PACKET_ID, RESERVED = 8, 0x1234, struct.pack("<I", 0xFACEC00D)
+    rng = random.Random(0x1234)
+    # build_from_memory with no content (:52-57)
+    mem = ro.build_packet(HEAD_SIZE, PACKET_ID, b"")
+    _check_packet(mem, 0, PACKET_ID, HEAD_SIZE, b"")
+    temp = bytes(rng.randrange(256) for _ in range(1024))
+    half = 512
+    _check_packet(ro.build_packet(HEAD_SIZE, PACKET_ID, temp[:half]), half, PACKET_ID, HEAD_SIZE, temp)  # :70-71
+    _check_packet(ro.build_packet(HEAD_SIZE, PACKET_ID, temp), 1024, PACKET_ID, HEAD_SIZE, temp)  # :77-78
+    _check_packet(ro.build_packet(HEAD_SIZE, PACKET_ID, temp[:half], temp[half:]), 1024, PACKET_ID, HEAD_SIZE,
+                  temp)  # two parts, :84-85
+    # build_from_ringbuf (:91-103): incomplete until head + size bytes are present
+    rb = bytearray()
+    assert ro.take_packet(rb, HEAD_SIZE) is None
+    rb += struct.pack(">HH", 1024, PACKET_ID) + RESERVED
+    assert ro.take_packet(rb, HEAD_SIZE) is None
+    rb += temp[:half]
+    assert ro.take_packet(rb, HEAD_SIZE) is None
+    rb += temp[half:]
+    mem = ro.take_packet(rb, HEAD_SIZE)
+    _check_packet(mem, 1024, PACKET_ID, HEAD_SIZE, temp)
+    assert mem[4:8] == RESERVED  # PACKET_CHECK_WITH_RESERVED, :26-28
+    # large packet, 0xFFFF bytes, whole and in two parts (:124-135)
+    big = bytes(rng.randrange(256) for _ in range(0xFFFF))
+    _check_packet(ro.build_packet(HEAD_SIZE, PACKET_ID, big), 0xFFFF, PACKET_ID, HEAD_SIZE, big)
+    _check_packet(ro.build_packet(HEAD_SIZE, PACKET_ID, big[:0x7FFF], big[0x7FFF:]), 0xFFFF, PACKET_ID, HEAD_SIZE,
+                  big)
+    assert ro.build_packet(HEAD_SIZE, PACKET_ID, big, b"x") is None  # over 0xFFFF builds nothing (cye_packet.cpp:117-118)
+    # The same ring-buffer sequence at the relay's head size (RELAY_PACKET_HEADSIZE = 4) through the product's parser.
+    rb = bytearray()
+    steps = [b"", struct.pack(">HH", 1024, PACKET_ID), temp[:half], temp[half:]]
+    for i, part in enumerate(steps):
+        rb += part
+        got, used = ca.relay_parse(bytes(rb))
+        want, wused = ro.parse_stream(bytes(rb))
+        assert (got, used) == (want, wused)
+        assert got == ([(0, 1024, PACKET_ID)] if i == len(steps) - 1 else [])
+    mem = ro.take_packet(rb, 4)
+    _check_packet(mem, 1024, PACKET_ID, 4, temp)
+
+
 def test_build_forward_rejects_oversize_chunk():
     with pytest.raises(ValueError):
         ca.relay_build_forward(1, bytes(0xFF01))
