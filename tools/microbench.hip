@@ -176,6 +176,51 @@ __global__ __launch_bounds__(1024, 1) void k_ldspeak(uint32_t* out, int iters, C
     }
 }
 
+// Cross-lane gathers: per iteration 16 lookups, NB of them ds_bpermute_b32
+// from a 256-B table held in one VGPR (lane l holds bytes 4l..4l+3: an S-box
+// fits), the rest conflict-free ds_read_b32.  Shows whether bpermute, which
+// reads no LDS bank, adds gather throughput beside the ds_read_b32 peak.
+template <int NB>
+__global__ __launch_bounds__(1024, 1) void k_bperm(uint32_t* out, int iters, Clk* clk) {
+    __shared__ uint32_t lds[24576];  // 96 KiB: one workgroup per CU
+    for (int i = threadIdx.x; i < 24576; i += blockDim.x) lds[i] = i * 2654435761u;
+    __syncthreads();
+    const uint32_t lo = (threadIdx.x & 31u) << 2;
+    const uint32_t tab = threadIdx.x * 0x01010101u + 0x03020100u;
+    uint32_t s[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) s[j] = (threadIdx.x * 7919u + j * 104729u) | 1;
+    unsigned long long t0 = 0, r0 = 0;
+    if (threadIdx.x == 0) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    for (int it = 0; it < iters; it++) {
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            if (j < NB) {
+                v[j] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s[j] >> (8 * (j & 3))) & 0xFCu), (int)tab);
+            } else {
+                const uint32_t a = __builtin_amdgcn_perm(s[j], lo, 0x0C0C0400u + ((j & 3) << 8));
+                v[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + a);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) s[j] ^= v[j];
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) acc ^= s[j];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+    if (threadIdx.x == 0) {
+        clk[blockIdx.x].t0 = t0;
+        clk[blockIdx.x].r0 = r0;
+        clk[blockIdx.x].t1 = __builtin_amdgcn_s_memtime();
+        clk[blockIdx.x].r1 = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // VALU issue: 8 independent chains x 8 unrolled ops of one kind.
 template <int OP>
 __global__ __launch_bounds__(1024, 1) void k_valu(uint32_t* out, int iters, Clk* clk) {
@@ -271,6 +316,13 @@ int main() {
     CHECK(hipMalloc(&d_tab, 1024));
     CHECK(hipMemset(d_tab, 0x5a, 1024));
     g_tab = d_tab;
+    if (getenv("MB_ONLY_BPERM")) {
+        run("bperm0_lds16", k_bperm<0>, 1024, it, 16, "lookups", cus, d_out, d_clk);
+        run("bperm4_lds12", k_bperm<4>, 1024, it, 16, "lookups", cus, d_out, d_clk);
+        run("bperm8_lds8", k_bperm<8>, 1024, it, 16, "lookups", cus, d_out, d_clk);
+        run("bperm16", k_bperm<16>, 1024, it, 16, "lookups", cus, d_out, d_clk);
+        return 0;
+    }
     // lane-ops per clk per CU (64 lanes x wave-instructions)
     run("valu_perm", k_valu<0>, 1024, it, 64, "lane-ops", cus, d_out, d_clk);
     run("valu_bitop3", k_valu<1>, 1024, it, 64, "lane-ops", cus, d_out, d_clk);
@@ -291,6 +343,10 @@ int main() {
     run("mix_vmem4", k_mix<4>, 1024, it, 16, "lookups", cus, d_out, d_clk);
     run("mix_vmem6", k_mix<6>, 1024, it, 16, "lookups", cus, d_out, d_clk);
     run("mix_vmem16", k_mix<16>, 1024, it / 4, 16, "lookups", cus, d_out, d_clk);
+    run("bperm0_lds16", k_bperm<0>, 1024, it, 16, "lookups", cus, d_out, d_clk);
+    run("bperm4_lds12", k_bperm<4>, 1024, it, 16, "lookups", cus, d_out, d_clk);
+    run("bperm8_lds8", k_bperm<8>, 1024, it, 16, "lookups", cus, d_out, d_clk);
+    run("bperm16", k_bperm<16>, 1024, it, 16, "lookups", cus, d_out, d_clk);
     CHECK(hipFree(d_tab));
     CHECK(hipFree(d_out));
     CHECK(hipFree(d_clk));
