@@ -524,6 +524,9 @@ void cyaes_batcher::complete_loop() {
         int status = st->status;
         const int64_t t0 = now_ns();
         if (status == CYAES_OK) status = map_err(hipEventSynchronize(st->done));
+        // A stage whose submit failed part-way may still have copies or kernels in
+        // flight on its buffers: drain its stream before the stage is reused.
+        if (status != CYAES_OK) (void)hipStreamSynchronize(st->stream);
         const int64_t t1 = now_ns();
         pc.sync += t1 - t0;
         if (status == CYAES_OK)

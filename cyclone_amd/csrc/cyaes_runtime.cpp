@@ -761,6 +761,9 @@ int dropin_run(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* o
         } catch (const std::bad_alloc&) {  // the slot and the waiters must still be released
             st = CYAES_ENOMEM;
         }
+        // A batch that failed part-way may still have copies in flight from the
+        // slot's pinned image: drain them before another leader refills it.
+        if (st && slot->stream) (void)hipStreamSynchronize(slot->stream);
         lk.lock();
         for (DropInCall* c : batch) {
             c->status = st;
