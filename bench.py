@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--packet-configs", default="B,D",
                     help="other BASELINE.json packet configs measured after the headline one ('none' to skip)")
     ap.add_argument("--packet-steps", type=int, default=20)
+    ap.add_argument("--packet-cpu-sample", type=int, default=262144,
+                    help="packet configs: payloads in the CPU-baseline sample (0 = auto)")
     ap.add_argument("--packet-warmup", type=int, default=20,
                     help="untimed steps before each packet config (a 1,472-B step is ~2 ms; 20 cover the clock "
                          "ramp, profiles/r01/packet_warmup.txt)")
@@ -472,13 +474,20 @@ def main():
     for name in ([] if args.packet_configs == "none" else args.packet_configs.split(",")):
         if name == args.config or name not in CONFIGS:
             continue
-        r = run_config(name, CONFIGS[name][0], args.packet_steps, args.packet_warmup, not args.no_verify)
+        want_cpu = rank == 0 and world == 1 and not args.no_cpu
+        r = run_config(name, CONFIGS[name][0], args.packet_steps, args.packet_warmup, not args.no_verify,
+                       keep_cipher=want_cpu)
+        pcpu = None
+        if want_cpu:  # the same config on the host cores, same run, a bounded sample
+            log("cpu baseline %s ..." % name)
+            pcpu = cpu_baseline(name, r["npay"], r["pb"], r["ppk"], r["d_ct"], torch, args.packet_cpu_sample)
+            r["d_ct"] = r["d_pt"] = None
         packet_configs[name] = {
             "value": round(r["value"], 2), "unit": "GiB/s", "ms_per_step": round(r["t"] / r["steps"] * 1e3, 4),
             "steps": r["steps"], "warmup": args.packet_warmup, "payloads_per_gpu": r["npay"], "payload_bytes": r["pb"],
             "payloads_per_key": r["ppk"], "encrypt_ms": round(r["enc_ms"], 4), "decrypt_ms": round(r["dec_ms"], 4),
             "hbm_frac_step": round(4.0 * r["nbytes"] / (r["t"] / r["steps"]) / 1e9 / HBM_PEAK_GBS, 4),
-            "parity": r["parity"], "shards": r["shards"],
+            "parity": r["parity"], "shards": r["shards"], "cpu_baseline": pcpu,
         }
         torch.cuda.empty_cache()
 
