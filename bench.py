@@ -86,8 +86,8 @@ def parse():
     ap.add_argument("--packet-configs", default="B,D",
                     help="other BASELINE.json packet configs measured after the headline one ('none' to skip)")
     ap.add_argument("--packet-steps", type=int, default=20)
-    ap.add_argument("--packet-cpu-sample", type=int, default=262144,
-                    help="packet configs: payloads in the CPU-baseline sample (0 = auto)")
+    ap.add_argument("--packet-cpu-sample", type=int, default=0,
+                    help="packet configs: payloads in the CPU-baseline sample (0 = auto: the whole 1,472-B batch)")
     ap.add_argument("--packet-warmup", type=int, default=20,
                     help="untimed steps before each packet config (a 1,472-B step is ~2 ms; 20 cover the clock "
                          "ramp, profiles/r01/packet_warmup.txt)")
