@@ -7,7 +7,8 @@ nothing is compiled, imported or executed).  Writes data, not source:
   ref_kat.json / ref_kat.txt  -- the Rijndael known-answer vector of
       test/unit/cyt_unit_crypt.cpp:177-186 (key, plaintext, ciphertext,
       iv_check), as hex; and (ref_kat.json "adler32") the Adler-32 known
-      answers of cyt_unit_crypt.cpp:18-50.
+      answers of cyt_unit_crypt.cpp:18-50, and ("ringbuf_checksum") the
+      RingBuf::checksum answers of cyt_unit_ring_buf.cpp:370-385.
   ref_tables.json             -- SHA-256 of each static table of
       source/cyCrypt/crypt/cyr_rijndael.cpp:25-501 (S, Si, T1..T8, U1..U4,
       rcon), serialised as little-endian u8/u32 arrays, plus DefaultIV
@@ -76,6 +77,25 @@ def adler_kat():
             "null_or_empty": 1, "random_cases": 100, "random_cap": 257}
 
 
+def ringbuf_checksum_kat():
+    """RingBuf::checksum known answers of test/unit/cyt_unit_ring_buf.cpp:370-385
+    (Adler-32 over byte ranges of the buffer holding text_pattern, :48-49) and
+    its empty / out-of-range rules (cyc_ring_buf.cpp:365-373), as data."""
+    src = open(os.path.join(REF, "test/unit/cyt_unit_ring_buf.cpp"), encoding="utf-8-sig").read()
+    text = re.search(r'const char\* text_pattern = "(.*?)";', src).group(1)
+    body = src[src.index("//checksum"):]
+    body = body[:body.index("//make wrap condition and checksum")]
+    cases = [{"off": 0 if o == "0" else int(o), "count": int(c), "adler": int(a, 16)}
+             for a, o, c in re.findall(r"REQUIRE_EQ\((0x[0-9a-fA-F]+)ul, rb1\.checksum\((\w+), (\d+)\)\)", body)]
+    full = int(re.search(r"REQUIRE_EQ\((0x[0-9a-fA-F]+)ul, rb1\.checksum\(0, text_length\)\)", body).group(1), 16)
+    hdr = open(os.path.join(REF, "source/cyCore/core/cyc_ring_buf.h"), encoding="utf-8-sig").read()
+    a, b = re.search(r"kDefaultCapacity = (\d+) - (\d+)", hdr).groups()
+    cap = int(a) - int(b)
+    assert len(cases) == 2
+    return {"source": "test/unit/cyt_unit_ring_buf.cpp:370-385; cyc_ring_buf.cpp:365-387", "text": text,
+            "full": full, "ranges": cases, "capacity": cap, "wrap_size": 32}
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not present; fixtures are committed, nothing to do")
@@ -86,6 +106,7 @@ def main():
         for name in ["key", "plaintext", "ciphertext", "iv_check"]:
             f.write("%s=%s\n" % (name, k[name]))
     k["adler32"] = adler_kat()
+    k["ringbuf_checksum"] = ringbuf_checksum_kat()
     with open(os.path.join(HERE, "ref_kat.json"), "w") as f:
         json.dump(k, f, indent=1)
     t = tables()

@@ -70,3 +70,39 @@ def test_large_buffer_and_split_property():
     assert b.value == want
     assert lib.cyaes_gpu_adler32(d.data_ptr(), 0, 0xdeadbeef, ctypes.byref(out), None) == 0 and out.value == 1
     ctx.close()
+
+
+def test_ringbuf_checksum_reference_kat_on_device():
+    """The RingBuf::checksum answers of the reference's own test
+    (test/unit/cyt_unit_ring_buf.cpp:370-401) from the device Adler-32: byte
+    ranges of "Hello,World!" in one batch, and a wrapped ring buffer as two
+    chained calls (the running value of the first piece seeds the second,
+    cyc_ring_buf.cpp:375-384)."""
+    import json
+    import os
+    import torch
+    k = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ref_kat.json")))["ringbuf_checksum"]
+    lib = _lib()
+    text = np.frombuffer(k["text"].encode(), dtype=np.uint8).copy()
+    d = torch.from_numpy(text).cuda()
+    cases = [(0, len(text), k["full"])] + [(c["off"], c["count"], c["adler"]) for c in k["ranges"]]
+    d_off = torch.tensor([c[0] for c in cases], dtype=torch.int64).cuda()
+    d_len = torch.tensor([c[1] for c in cases], dtype=torch.int64).cuda()
+    d_out = torch.empty(len(cases), dtype=torch.int32).cuda()
+    assert lib.cyaes_gpu_adler32_batch(d.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), None, d_out.data_ptr(),
+                                       len(cases), None) == 0
+    got = d_out.cpu().numpy().view(np.uint32)
+    assert [int(x) for x in got] == [c[2] for c in cases]
+    # wrap: ring of capacity + 1 bytes (cyc_ring_buf.cpp:20), data from read = end - w, 4w bytes
+    rng = random.Random(7)
+    w = k["wrap_size"]
+    ring = np.frombuffer(bytes(rng.getrandbits(8) for _ in range(k["capacity"] + 1)), dtype=np.uint8).copy()
+    dr = torch.from_numpy(ring).cuda()
+    read = len(ring) - w
+    stream = np.concatenate([ring[read:], ring[:3 * w]])
+    a = ctypes.c_uint32()
+    b = ctypes.c_uint32()
+    assert lib.cyaes_gpu_adler32(dr.data_ptr() + read, w, 1, ctypes.byref(a), None) == 0
+    assert lib.cyaes_gpu_adler32(dr.data_ptr(), 2 * w, a.value, ctypes.byref(b), None) == 0
+    assert b.value == oracle.adler32(1, stream[:3 * w].tobytes())
+

@@ -162,6 +162,46 @@ def test_adler32_oracle_reference_kat(golden):
     assert oracle.adler32(oracle.adler32(1, data[:first]), data[first:]) == k["data_adler"]
 
 
+def ringbuf_checksum(ring, read, size, off, count):
+    """RingBuf::checksum (cyc_ring_buf.cpp:365-387) over a ring of len(ring)
+    bytes holding `size` bytes from index `read`: Adler-32 chained over the
+    (at most two) contiguous pieces; an empty or out-of-range request returns
+    INITIAL_ADLER."""
+    adler = 1
+    if off > size or off + count > size or count == 0:
+        return adler
+    pos, done = (read + off) % len(ring), 0
+    while done != count:
+        n = min(len(ring) - pos, count - done)
+        adler = oracle.adler32(adler, bytes(ring[pos:pos + n]))
+        pos, done = (pos + n) % len(ring), done + n
+    return adler
+
+
+def test_ringbuf_checksum_reference_kat(golden):
+    """RingBuf::checksum answers of the reference's own test
+    (test/unit/cyt_unit_ring_buf.cpp:370-401) on the oracle's Adler-32."""
+    k = golden["kat"]["ringbuf_checksum"]
+    text = k["text"].encode()
+    ring = bytearray(k["capacity"] + 1)  # m_end = capacity + 1 (cyc_ring_buf.cpp:20)
+    ring[:len(text)] = text
+    n = len(text)
+    assert ringbuf_checksum(ring, 0, n, 0, n) == k["full"]
+    for c in k["ranges"]:
+        assert ringbuf_checksum(ring, 0, n, c["off"], c["count"]) == c["adler"]
+    for off, count in [(n, 0), (n, 1), (0, n + 1), (0, 0)]:  # :375-378
+        assert ringbuf_checksum(ring, 0, n, off, count) == 1
+    # wrap (:387-401): the buffer's bytes [read, end) then [0, ...) chain as one stream
+    rng = random.Random(7)
+    w = k["wrap_size"]
+    ring = bytearray(rng.getrandbits(8) for _ in range(k["capacity"] + 1))
+    read = len(ring) - w
+    size = 4 * w
+    stream = bytes(ring[read:]) + bytes(ring[:size - w])
+    for off, count in [(0, w), (0, 3 * w), (2 * w, w), (3 * w, w)]:
+        assert ringbuf_checksum(ring, read, size, off, count) == oracle.adler32(1, stream[off:off + count])
+
+
 def test_adler32_oracle_random_split_and_zlib():
     """cyt_unit_crypt.cpp:54-78 (random split property) and, independently,
     zlib's adler32 (same algorithm) for every length class of the reference's
