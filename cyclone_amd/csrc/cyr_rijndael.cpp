@@ -9,8 +9,6 @@ namespace cyclone {
 const Rijndael::BLOCK Rijndael::DefaultIV = {0x00, 0x01, 0x02, 0x03, 0x04, 0x05, 0x06, 0x07,
                                              0x08, 0x09, 0x0a, 0x0b, 0x0c, 0x0d, 0x0e, 0x0f};
 
-Rijndael::Rijndael(const BLOCK key) : m_status(CYAES_OK) { m_status = cyaes_key_expand(key, &m_key); }
-
 Rijndael::~Rijndael() {}
 
 // Fails closed.  The reference's scalar encrypt cannot fail, and the relay
@@ -24,6 +22,14 @@ Rijndael::~Rijndael() {}
     fprintf(stderr, "cyclone::Rijndael::%s: %s (status %d); aborting rather than leave the buffer unprocessed\n",
             what, cyaes_strerror(status), status);
     abort();
+}
+
+// A key that cannot be expanded (NULL; the reference dereferences it,
+// cyr_rijndael.cpp:526-534) would leave a schedule that encrypts with the
+// wrong key: fail closed here too.
+Rijndael::Rijndael(const BLOCK key) : m_status(CYAES_OK) {
+    m_status = cyaes_key_expand(key, &m_key);
+    if (m_status != CYAES_OK) fail("Rijndael", m_status);
 }
 
 void Rijndael::encrypt(const uint8_t* input, uint8_t* output, size_t size, BLOCK iv) {
