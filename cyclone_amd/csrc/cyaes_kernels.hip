@@ -46,6 +46,9 @@
 #ifndef CYAES_RAGGED_REGULAR
 #define CYAES_RAGGED_REGULAR 1  // ragged decrypt: strided equal-size payload groups walk positions per lane
 #endif
+#ifndef CYAES_RAGGED_PRIO_LATE
+#define CYAES_RAGGED_PRIO_LATE 1  // ragged decrypt: progress atomic after the step's loads
+#endif
 #ifndef CYAES_TAIL_PREFETCH
 #define CYAES_TAIL_PREFETCH 1  // encrypt: prefetch a payload's partial last chunk with the chunk before
 #endif
@@ -969,7 +972,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         const uint64_t total = regular ? (uint64_t)gn * nb0 : rlane64(incl, 63);  // lanes >= gn add 0
         uint4 carry = make_uint4(0, 0, 0, 0);
         for (uint64_t base = 0; base < total; base += 64 * R) {
-            prio_feedback(leadp, ++prog, kDecPrioDiv);
+            if (!CYAES_RAGGED_PRIO_LATE) prio_feedback(leadp, ++prog, kDecPrioDiv);
             uint4 c[R], pv[R];
             uint32_t jr[R], rr[R];
             uint64_t orow[R];
@@ -1026,6 +1029,10 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
             const uint64_t safe = rlane64(orow[0], 0);
 #pragma unroll
             for (int k = 0; k < R; k++) c[k] = ldu(a.in + (valid[k] ? orow[k] : safe));
+            // The progress atomic (a global word: the decrypt image fills the LDS) goes
+            // out after the step's loads, so its round trip overlaps theirs instead of
+            // delaying them (A/B: -1 % on relay streams, profiles/r02/ab_ragged_prio_late.txt).
+            if (CYAES_RAGGED_PRIO_LATE) prio_feedback(leadp, ++prog, kDecPrioDiv);
             pv[0] = shr1(c[0], carry);
 #pragma unroll
             for (int k = 1; k < R; k++)
