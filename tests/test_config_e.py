@@ -115,3 +115,35 @@ def test_two_rank_session_keys_bit_exact():
         mine = [keys[16 * k:16 * k + 16] for k in range(p0 // ppk, (p0 + n) // ppk)]
         ct = oracle.batch(False, mine, ppk, oracle.synthetic(p0, n, pb), pb, nthreads=8)
         assert ["%016x" % v for v in oracle.digest(ct)] == sh["cipher_digest"], sh["rank"]
+
+
+@pytest.mark.gpu
+def test_bench_line_contract_single_gpu():
+    """bench.py at N = 1 as the driver runs it (fresh child process), on reduced
+    config E passes and a reduced packet config: one JSON line on stdout with
+    every field the bench contract names, the roofline and CPU-baseline
+    objects, per-pass parity against the committed digests, and the packet
+    config's own same-run CPU baseline, bit-identical to the GPU output."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", "E", "--e-pass-payloads", "4096",
+           "--e-passes", "2", "--steps", "2", "--warmup", "1", "--packet-configs", "B", "--packet-steps", "2",
+           "--packet-warmup", "1", "--cpu-sample", "512", "--packet-cpu-sample", "4096", "--no-clock"]
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout[-2000:]
+    out = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "parity"):
+        assert k in out, k
+    assert out["metric"].startswith("AES encrypt+decrypt GiB/s") and out["unit"] == "GiB/s"
+    assert out["n_gpus"] == 1 and out["steps"] == 2 and out["warmup"] == 1 and out["higher_is_better"] is True
+    assert out["value"] > 0 and out["ms_per_step"] > 0 and out["parity"] == "bit-exact"
+    assert out["config"]["workload"].startswith("config E") and out["config"]["passes_per_gpu"] == 2
+    assert out["shards"][0]["golden_verified"] == [0, 1]
+    r = out["roofline"]
+    assert r["bound"] == "lds" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3 and r["traffic"] > 0
+    c = out["cpu_baseline"]
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["matches_gpu"] is True and c["sample"]
+    b = out["packet_configs"]["B"]
+    assert b["parity"] == "bit-exact" and b["payload_bytes"] == 1472 and b["cpu_baseline"]["matches_gpu"] is True
