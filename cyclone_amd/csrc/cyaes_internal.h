@@ -47,7 +47,10 @@ constexpr int kDecWgPerCu = 1;
 #endif
 constexpr uint64_t kQuadRaggedFactor = 16;
 // Decrypt: blocks per lane per step (a wave step covers 64*kDecRows blocks).
-constexpr int kDecRows = 4;
+#ifndef CYAES_DEC_ROWS
+#define CYAES_DEC_ROWS 4
+#endif
+constexpr int kDecRows = CYAES_DEC_ROWS;
 
 struct Fastdiv {  // Lemire: q = mulhi64(M, n) exact for all 32-bit n, d >= 2
     uint64_t M;
