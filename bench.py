@@ -181,11 +181,17 @@ def main():
     device = 0 if os.environ.get("CYAES_BENCH_SAME_DEVICE") else local
     backend = os.environ.get("CYAES_DIST_BACKEND", "nccl")
     torch.cuda.set_device(device)
-    if world > 1:
+    # CYAES_BENCH_FORCE_DIST=1 initialises the process group even at world size 1,
+    # so the driver's N>1 code path (RCCL init on the rank's device, key
+    # broadcast, barriers, max-over-ranks all_reduce, shard all_gather) runs on a
+    # one-GPU box (tests/test_config_e.py).
+    dist_on = world > 1 or bool(os.environ.get("CYAES_BENCH_FORCE_DIST"))
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group(backend)
+        log("process group: backend %s, world %d, device %d" % (dist.get_backend(), dist.get_world_size(), device))
 
     import cyclone_amd as ca
     from cyclone_amd import dist as cdist
@@ -198,13 +204,13 @@ def main():
 
     def max_over_ranks(x):
         v = torch.tensor([x], dtype=torch.float64, device="cuda")
-        if world > 1:
+        if dist_on:
             dist.all_reduce(v, op=dist.ReduceOp.MAX)
         return float(v.item())
 
     def all_ok(ok):
         flag = torch.tensor([0 if ok else 1], device="cuda")
-        if world > 1:
+        if dist_on:
             dist.all_reduce(flag)
         return int(flag.item()) == 0
 
@@ -260,13 +266,13 @@ def main():
             shard["cipher_digest"] = ["%016x" % v for v in ctx.digest(d_ct, nbytes, sh)]
             log("config %s parity: %s" % (name, parity))
         shards = [shard]
-        if world > 1:
+        if dist_on:
             shards = [None] * world
             dist.all_gather_object(shards, shard)
 
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
                torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -277,7 +283,7 @@ def main():
             dec()
             ev[i][2].record(stream)
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         t1 = time.perf_counter()
         t = max_over_ranks(t1 - t0)
@@ -346,7 +352,7 @@ def main():
         ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
                 torch.cuda.Event(enable_timing=True)) for _ in mine] for _ in range(steps)]
         t_aes, t_fill = 0.0, 0.0
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         t_begin = time.perf_counter()
@@ -366,12 +372,12 @@ def main():
                 t_fill += a0 - f0
                 t_aes += a1 - a0
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         t_wall = time.perf_counter() - t_begin
         t = max_over_ranks(t_aes)
         shards = None
-        if world > 1:
+        if dist_on:
             shards = [None] * world
             dist.all_gather_object(shards, {"rank": rank, "passes": mine, "golden_verified": verified})
         else:
@@ -524,7 +530,7 @@ def main():
                                       "max over ranks", "fill_ms_per_step": round(main_res["fill_ms"], 3),
                              "wall_ms_per_step_incl_fill": round(main_res["wall_ms"], 3)}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     ctx.close()
 

@@ -48,6 +48,6 @@ def broadcast_keys(keys, nkeys, device, src=0, group=None):
         t = torch.frombuffer(bytearray(keys), dtype=torch.uint8).to(device)
     else:
         t = torch.zeros(16 * nkeys, dtype=torch.uint8, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.broadcast(t, src=src, group=group)
     return t

@@ -147,3 +147,28 @@ def test_bench_line_contract_single_gpu():
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["matches_gpu"] is True and c["sample"]
     b = out["packet_configs"]["B"]
     assert b["parity"] == "bit-exact" and b["payload_bytes"] == 1472 and b["cpu_baseline"]["matches_gpu"] is True
+
+
+@pytest.mark.gpu
+def test_rccl_path_world_one_bit_exact():
+    """The driver's N>1 code path on RCCL itself: bench.py under torchrun with
+    the default backend ("nccl" = RCCL) at world size 1 (CYAES_BENCH_FORCE_DIST
+    initialises the process group anyway).  RCCL init on the rank's device, the
+    session-key broadcast into device memory, barriers, the max-over-ranks
+    all_reduce and the shard all_gather all run on the GPU; config E passes and
+    the per-session-key config D stay bit-exact against their committed digests."""
+    env = dict(os.environ, CYAES_BENCH_FORCE_DIST="1", OMP_NUM_THREADS="4")
+    env.pop("CYAES_DIST_BACKEND", None)
+    env.pop("CYAES_BENCH_SAME_DEVICE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", "E", "--e-pass-payloads", "4096",
+           "--e-passes", "2", "--steps", "2", "--warmup", "1", "--packet-configs", "D", "--packet-steps", "2",
+           "--packet-warmup", "1", "--no-cpu", "--no-clock"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=130)
+    assert p.returncode == 0, p.stderr[-4000:]
+    assert "process group: backend nccl, world 1" in p.stderr, p.stderr[-4000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["parity"] == "bit-exact" and out["n_gpus"] == 1
+    assert out["shards"][0]["golden_verified"] == [0, 1]
+    assert out["packet_configs"]["D"]["parity"] == "bit-exact"
