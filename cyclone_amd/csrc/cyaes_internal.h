@@ -38,14 +38,18 @@ constexpr int kEncWgPerCu = 1;
 constexpr int kDecThreads = 1024;
 constexpr int kDecWgPerCu = 1;
 // Uniform encrypt batches with fewer chains than this run four lanes per
-// chain (k_encrypt_quad), larger ones one lane per chain (k_encrypt); ragged
-// batches switch at kQuadRaggedFactor times the count, because relay packets
-// (payload at packet offset 12) are not 16-B aligned and the quad kernel's
-// dword accesses lose less to that (tools/ab_quad.py, tools/ab_ragged.py).
+// chain (k_encrypt_quad), larger ones one lane per chain (k_encrypt).  Ragged
+// batches switch at kQuadRaggedFactor times the count.  It was 16 while the
+// lane kernel waited for each chunk's stores before its next loads (relay
+// packets, payload at packet offset 12, then took 1.80 ms per 1 M in place
+// against the quad kernel's 1.50); with one prefetch path it no longer does,
+// and on relay streams the lane kernel wins from 131,072 packets up (0.206 vs
+// 0.223 ms; 1 M: 1.30 vs 1.51 ms) and loses below (65,536: 0.149 vs 0.114)
+// (scripts/ab_ragged_switch.sh, profiles/r02/ab_ragged_switch.txt).
 #ifndef CYAES_QUAD_MAX_CHAINS
 #define CYAES_QUAD_MAX_CHAINS 131072
 #endif
-constexpr uint64_t kQuadRaggedFactor = 16;
+constexpr uint64_t kQuadRaggedFactor = 1;
 // Decrypt: blocks per lane per step (a wave step covers 64*kDecRows blocks).
 #ifndef CYAES_DEC_ROWS
 #define CYAES_DEC_ROWS 4

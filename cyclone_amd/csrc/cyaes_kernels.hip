@@ -49,6 +49,9 @@
 #ifndef CYAES_RAGGED_PRIO_LATE
 #define CYAES_RAGGED_PRIO_LATE 1  // ragged decrypt: progress atomic after the step's loads
 #endif
+#ifndef CYAES_ENC_ONE_PREFETCH
+#define CYAES_ENC_ONE_PREFETCH 1  // encrypt: one prefetch path for full and partial next chunks (A/B: 0 = two paths)
+#endif
 #ifndef CYAES_TAIL_PREFETCH
 #define CYAES_TAIL_PREFETCH 1  // encrypt: prefetch a payload's partial last chunk with the chunk before
 #endif
@@ -457,6 +460,18 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                     const bool tail = CYAES_TAIL_PREFETCH && !CYAES_NO_PREFETCH && !more && i + 8 < nb;  // partial last chunk
 #if !CYAES_NO_PREFETCH  // A/B: -8% encrypt time vs loading at the top of the chunk
                     uint4 bn[8];  // next chunk's loads in flight during this chunk's rounds
+#if CYAES_ENC_ONE_PREFETCH
+                    if (more || tail) {
+                        // One set of 8 loads for both cases: a partial last chunk loads
+                        // the payload's last 8 blocks (its tail then sits at the top of
+                        // bn).  With every bn[j] defined on this path the compiler no
+                        // longer waits for this chunk's stores (s_waitcnt vmcnt(0))
+                        // before the next chunk's loads; it waits only for the loads.
+                        const uint8_t* nsrc = src + 16ull * (more ? i + 8 : nb - 8);
+#pragma unroll
+                        for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(nsrc, j);
+                    }
+#else
                     if (more) {
 #pragma unroll
                         for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(src, i + 8 + j);
@@ -465,6 +480,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                         for (int j = 0; j < 7; j++)
                             if (i + 8 + j < nb) bn[j] = ldb<RAGGED>(src, i + 8 + j);
                     }
+#endif
 #endif
                     prio_feedback(&lead, ++prog, kEncPrioDiv);
 #pragma unroll
@@ -490,6 +506,17 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                     have_tail = tail;
 #endif
                 }
+#if CYAES_ENC_ONE_PREFETCH
+                if (have_tail) {  // the tail's nb - i blocks sit in b[8 - (nb - i), 8): move them down to b[0]
+#pragma unroll
+                    for (int sft = 1; sft < 8; sft++) {
+                        if (sft <= 8 - (int)(nb - i)) {
+#pragma unroll
+                            for (int j = 0; j < 7; j++) b[j] = b[j + 1];
+                        }
+                    }
+                }
+#endif
                 for (; i < nb; i++) {  // partial last chunk: from b (prefetched) or loaded here
                     const uint4 v = have_tail ? b[0] : ldb<RAGGED>(src, i);
 #pragma unroll

@@ -4,7 +4,8 @@
 Times cyaes_gpu_encrypt_ragged on N equal payloads under layouts that differ in
 one property at a time: packet stride (payload + header bytes), payload offset
 inside the packet (12 = relay, 16 = 16-B aligned) and in place vs a separate
-output stream.  usage: python tools/ab_relay_layout.py [--n 1048576] [--pb 1472]"""
+output stream.  usage: python tools/ab_relay_layout.py [--n 1048576] [--pb 1472]
+[--lib a.so [b.so ...]] [--layouts relay_inplace,...]  (several libs: interleaved per round, one process)"""
 import argparse
 import os
 import statistics
@@ -19,13 +20,17 @@ def main():
     ap.add_argument("--n", type=int, default=1048576)
     ap.add_argument("--pb", type=int, default=1472)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--lib", default=None)
+    ap.add_argument("--lib", nargs="*", default=None)
+    ap.add_argument("--layouts", default=None, help="comma-separated subset of the layout labels")
     args = ap.parse_args()
     import numpy as np
     import torch
     import cyclone_amd as ca
-    c = ca.GpuContext(0, lib=ca.load_library(os.path.abspath(args.lib)) if args.lib else None)
-    c.set_keys(bytes(range(16)))
+    libs = args.lib or [None]
+    ctxs = [ca.GpuContext(0, lib=ca.load_library(os.path.abspath(p)) if p else None) for p in libs]
+    for c in ctxs:
+        c.set_keys(bytes(range(16)))
+    c = ctxs[0]
     s = torch.cuda.current_stream()
     n, pb = args.n, args.pb
     pt = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
@@ -38,25 +43,32 @@ def main():
                ("hdr16_out", 16, pb + 16, False), ("hdr16_inplace", 16, pb + 16, True),
                ("hdr12_s1488_out", 12, pb + 16, False), ("hdr12_s1488_inplace", 12, pb + 16, True),
                ("relay_out", 12, pb + 12, False), ("relay_inplace", 12, pb + 12, True)]
+    if args.layouts:
+        keep = args.layouts.split(",")
+        layouts = [ly for ly in layouts if ly[0] in keep]
     for label, hdr, stride, inplace in layouts:
         src = torch.zeros(n * stride + 16, dtype=torch.uint8, device="cuda")
         src[: n * stride].view(n, stride)[:, hdr:hdr + pb] = pt.view(n, pb)
         dst = src if inplace else torch.zeros_like(src)
         off = torch.from_numpy(np.arange(n, dtype=np.uint64) * stride + hdr).to("cuda")
-        ts = []
+        ts = [[] for _ in ctxs]
+        ok = [True for _ in ctxs]
         for r in range(args.rounds + 1):
-            if inplace:
-                src[: n * stride].view(n, stride)[:, hdr:hdr + pb] = pt.view(n, pb)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            c.encrypt_ragged(src, dst, off, nb, n, stream=s.cuda_stream)
-            e1.record(s)
-            torch.cuda.synchronize()
-            if r:
-                ts.append(e0.elapsed_time(e1))
-        ok = torch.equal(dst[: n * stride].view(n, stride)[:, hdr:hdr + pb].reshape(-1), ref)
-        print("%-22s %8d x %5d B stride %5d: enc %.4f ms (min %.4f)  %s" %
-              (label, n, pb, stride, statistics.median(ts), min(ts), "ok" if ok else "MISMATCH"), flush=True)
+            for k, ck in enumerate(ctxs):
+                if inplace:
+                    src[: n * stride].view(n, stride)[:, hdr:hdr + pb] = pt.view(n, pb)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                ck.encrypt_ragged(src, dst, off, nb, n, stream=s.cuda_stream)
+                e1.record(s)
+                torch.cuda.synchronize()
+                if r:
+                    ts[k].append(e0.elapsed_time(e1))
+                ok[k] = ok[k] and torch.equal(dst[: n * stride].view(n, stride)[:, hdr:hdr + pb].reshape(-1), ref)
+        for k, p in enumerate(libs):
+            print("%-22s %8d x %5d B stride %5d: enc %.4f ms (min %.4f)  %s  %s" %
+                  (label, n, pb, stride, statistics.median(ts[k]), min(ts[k]), "ok" if ok[k] else "MISMATCH",
+                   os.path.basename(p) if p else ""), flush=True)
         del src, dst
         torch.cuda.empty_cache()
 
