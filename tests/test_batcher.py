@@ -391,3 +391,37 @@ def test_submit_many_mixed_ops_order_and_errors(batcher):
             assert bytes(rec["out"]) == ro.open_forward(keys[rec["k"]], rec["sealed"])[2]
     for s in slots:
         batcher.session_close(s)
+
+
+def test_device_relay_stream_config_b_default_kernels():
+    """Config B's 1 M payloads as a relay packet stream in HBM (payload at packet
+    offset 12, packet stride 1,484 B: 4-B aligned, relay_protocol.h:5-42), encrypted
+    and decrypted in place with the runtime's default kernel choice -- one lane per
+    chain from 131,072 ragged chains up (cyaes_internal.h kQuadRaggedFactor).  The
+    gathered ciphertext's digest equals config B's committed OpenSSL digest
+    (tests/golden/openssl_vectors.json), the packet headers stay untouched, and
+    decrypt restores the plaintext."""
+    import json
+    import os
+    import torch
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "openssl_vectors.json")))["configs"]["B"]
+    n, pb, hdr, stride = g["npayloads"], g["payload_bytes"], 12, g["payload_bytes"] + 12
+    ctx = ca.GpuContext(0)
+    ctx.set_keys(bytes(range(16)))
+    pt = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
+    ctx.fill_synthetic(pt, 0, n, pb, 0x5EEDC1C1)
+    assert ["%016x" % v for v in ctx.digest(pt, n * pb)] == g["plain_digest"]
+    buf = torch.full((n * stride + 16,), 0xA5, dtype=torch.uint8, device="cuda")
+    view = buf[: n * stride].view(n, stride)
+    view[:, hdr:hdr + pb] = pt.view(n, pb)
+    off = (torch.arange(n, dtype=torch.int64, device="cuda") * stride + hdr).contiguous()
+    nb = torch.full((n,), pb, dtype=torch.int32, device="cuda")
+    ctx.encrypt_ragged(buf, buf, off, nb, n)
+    assert ctx.check() == ca.CYAES_OK
+    ct = view[:, hdr:hdr + pb].contiguous()
+    assert ["%016x" % v for v in ctx.digest(ct, n * pb)] == g["cipher_digest"]
+    assert bool((view[:, :hdr] == 0xA5).all()) and bool((buf[n * stride:] == 0xA5).all())
+    ctx.decrypt_ragged(buf, buf, off, nb, n)
+    assert ctx.check() == ca.CYAES_OK
+    assert torch.equal(view[:, hdr:hdr + pb].reshape(-1), pt)
+    ctx.close()
