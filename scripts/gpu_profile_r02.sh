@@ -18,7 +18,7 @@ step() {  # step NAME SECONDS CMD...
 }
 cd /tmp
 step counters 60 rocprofv3 -L
-step rocprof_stats 300 rocprofv3 --kernel-trace --stats -d "$O/rocprof" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --packet-configs none
-step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" --config C --steps 2 --warmup 0 --no-cpu --no-verify --no-clock --packet-configs none
-step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" --config C --steps 2 --warmup 0 --no-cpu --no-verify --no-clock --packet-configs none
+step rocprof_stats 300 rocprofv3 --kernel-trace --stats -d "$O/rocprof" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --packet-configs none --relay-stream 0
+step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" --config C --steps 2 --warmup 0 --no-cpu --no-verify --no-clock --packet-configs none --relay-stream 0
+step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" --config C --steps 2 --warmup 0 --no-cpu --no-verify --no-clock --packet-configs none --relay-stream 0
 echo "[gpu] done"

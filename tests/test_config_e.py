@@ -75,7 +75,8 @@ def test_two_rank_config_e_bit_exact(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "E", "--e-pass-payloads", "4096",
-           "--e-passes", "8", "--steps", "2", "--warmup", "1", "--packet-configs", "none", "--no-cpu", "--no-clock"]
+           "--e-passes", "8", "--steps", "2", "--warmup", "1", "--packet-configs", "none", "--no-cpu", "--no-clock",
+           "--relay-stream", "0"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=130)
     (tmp_path / "stderr.txt").write_text(p.stderr)
     assert p.returncode == 0, p.stderr[-4000:]
@@ -103,7 +104,8 @@ def test_two_rank_session_keys_bit_exact():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "D", "--payloads", str(per_rank),
-           "--steps", "2", "--warmup", "1", "--packet-configs", "none", "--no-cpu", "--no-clock"]
+           "--steps", "2", "--warmup", "1", "--packet-configs", "none", "--no-cpu", "--no-clock",
+           "--relay-stream", "0"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=130)
     assert p.returncode == 0, p.stderr[-4000:]
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
@@ -147,6 +149,8 @@ def test_bench_line_contract_single_gpu():
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["matches_gpu"] is True and c["sample"]
     b = out["packet_configs"]["B"]
     assert b["parity"] == "bit-exact" and b["payload_bytes"] == 1472 and b["cpu_baseline"]["matches_gpu"] is True
+    r = out["relay_stream"]  # config B's payloads as an in-place relay packet stream, vs config B's digest
+    assert r["parity"] == "bit-exact" and r["value"] > 0 and r["encrypt_ms"] > 0 and r["decrypt_ms"] > 0
 
 
 @pytest.mark.gpu
@@ -172,3 +176,4 @@ def test_rccl_path_world_one_bit_exact():
     assert out["parity"] == "bit-exact" and out["n_gpus"] == 1
     assert out["shards"][0]["golden_verified"] == [0, 1]
     assert out["packet_configs"]["D"]["parity"] == "bit-exact"
+    assert out["relay_stream"]["parity"] == "bit-exact"
