@@ -49,6 +49,9 @@
 #ifndef CYAES_RAGGED_PRIO_LATE
 #define CYAES_RAGGED_PRIO_LATE 1  // ragged decrypt: progress atomic after the step's loads
 #endif
+#ifndef CYAES_RAGGED_ALIGNED_STORES
+#define CYAES_RAGGED_ALIGNED_STORES 0  // ragged lane encrypt: 16-B aligned window stores (A/B)
+#endif
 #ifndef CYAES_ENC_ONE_PREFETCH
 #define CYAES_ENC_ONE_PREFETCH 1  // encrypt: one prefetch path for full and partial next chunks (A/B: 0 = two paths)
 #endif
@@ -373,6 +376,28 @@ __device__ __forceinline__ void stb(uint8_t* base, uint32_t i, uint4 v) {
     else reinterpret_cast<uint4*>(base)[i] = v;
 }
 
+#if CYAES_RAGGED_ALIGNED_STORES
+// Ragged encrypt, 4-B aligned payloads (A/B): store 16-B aligned windows
+// instead of 4-B aligned blocks.  With the payload mis words past a 16-B
+// boundary, window k holds the last mis words of block k-1 and the first
+// 4 - mis words of block k: S = prev | cur (8 words), window = S[4-mis, 8-mis),
+// picked in two select stages (shift by 1 word, then by 2).
+__device__ __forceinline__ uint4 awin(uint4 prev, uint4 cur, uint32_t mis) {
+    const bool s1 = mis & 1u, s2 = mis & 2u;
+    const uint32_t t2 = s1 ? prev.y : prev.z, t3 = s1 ? prev.z : prev.w, t4 = s1 ? prev.w : cur.x;
+    const uint32_t t5 = s1 ? cur.x : cur.y, t6 = s1 ? cur.y : cur.z, t7 = s1 ? cur.z : cur.w;
+    return make_uint4(s2 ? t2 : t4, s2 ? t3 : t5, s2 ? t4 : t6, s2 ? t5 : t7);
+}
+// Words [from, to) of window w at the 16-B aligned p (the payload's first and last windows).
+__device__ __forceinline__ void awin_part(uint8_t* p, uint4 w, uint32_t from, uint32_t to) {
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    if (from <= 0 && 0 < to) q[0] = w.x;
+    if (from <= 1 && 1 < to) q[1] = w.y;
+    if (from <= 2 && 2 < to) q[2] = w.z;
+    if (from <= 3 && 3 < to) q[3] = w.w;
+}
+#endif
+
 __device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kIv2, kIv3); }
 
 #if CYAES_CLOCK_PROBE
@@ -448,6 +473,11 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                 uint4 c = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
                 const uint8_t* src = a.in + off;  // ragged: 4-B aligned
                 uint8_t* dst = a.out + off;
+#if CYAES_RAGGED_ALIGNED_STORES
+                const uint32_t mis = RAGGED ? (uint32_t)(((uintptr_t)dst & 15u) >> 2) : 0u;
+                uint8_t* const adst = dst - 4u * mis;  // 16-B aligned
+                uint4 carry = make_uint4(0, 0, 0, 0);  // the previous block (its last mis words go out with the next)
+#endif
                 uint32_t i = 0;
                 uint4 b[8];
                 if (nb >= 8) {
@@ -491,9 +521,22 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                         c = make_uint4(s0, s1, s2, s3);
                         b[j] = c;
                     }
+#if CYAES_RAGGED_ALIGNED_STORES
+                    if (RAGGED) {
+                        uint8_t* const ac = adst + 16ull * i;
+                        const uint4 w0 = awin(carry, b[0], mis);
+                        if (i == 0) awin_part(ac, w0, mis, 4);
+                        else *reinterpret_cast<uint4*>(ac) = w0;
+#pragma unroll
+                        for (int j = 1; j < 8; j++) *reinterpret_cast<uint4*>(ac + 16 * j) = awin(b[j - 1], b[j], mis);
+                        carry = b[7];
+                    } else
+#endif
+                    {
                     uint8_t* const dchunk = dst + 16ull * i;  // one address, immediate offsets (ragged too)
 #pragma unroll
                     for (int j = 0; j < 8; j++) stb<RAGGED>(dchunk, j, b[j]);  // (nt stores measured 3.6x slower)
+                    }
 #if CYAES_NO_PREFETCH
                     if (more) {
 #pragma unroll
@@ -526,8 +569,20 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                     uint32_t s2 = xor3(c.z, v.z, ek[2]), s3 = xor3(c.w, v.w, ek[3]);
                     enc_block(lds, lo, ek, s0, s1, s2, s3);
                     c = make_uint4(s0, s1, s2, s3);
+#if CYAES_RAGGED_ALIGNED_STORES
+                    if (RAGGED) {
+                        const uint4 w = awin(carry, c, mis);
+                        if (i == 0) awin_part(adst, w, mis, 4);
+                        else *reinterpret_cast<uint4*>(adst + 16ull * i) = w;
+                        carry = c;
+                        continue;
+                    }
+#endif
                     stb<RAGGED>(dst, i, c);
                 }
+#if CYAES_RAGGED_ALIGNED_STORES
+                if (RAGGED && nb > 0 && mis > 0) awin_part(adst + 16ull * nb, awin(carry, carry, mis), 0, mis);
+#endif
                 if (a.iv_out) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c;
             }
         }
