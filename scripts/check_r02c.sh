@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$PWD}
 O=$R/gpurun_out/${1:-check_c}
 mkdir -p "$O"
 cd "$R"
-timeout -k 10 200 python -u -m pytest tests/test_config_e.py -m gpu -v --timeout 150 --timeout-method thread -k rccl > "$O/pytest_rccl.txt" 2>&1
+CYAES_TEST_RCCL=1 timeout -k 10 200 python -u -m pytest tests/test_config_e.py -m gpu -v --timeout 150 --timeout-method thread -k rccl > "$O/pytest_rccl.txt" 2>&1
 rc=$?; tail -2 "$O/pytest_rccl.txt"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 480 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > "$O/pytest_gpu.txt" 2>&1
 rc=$?; tail -2 "$O/pytest_gpu.txt"; [ $rc -ne 0 ] && exit $rc

@@ -154,6 +154,10 @@ def test_bench_line_contract_single_gpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.skipif(not os.environ.get("CYAES_TEST_RCCL"),
+                    reason="opt-in (CYAES_TEST_RCCL=1): a second process initialising RCCL on the device the "
+                           "test process holds; two GPU-suite runs with it in the default set later reported "
+                           "illegal-address errors in runtime copies (DESIGN.md §4), so it runs on its own")
 def test_rccl_path_world_one_bit_exact():
     """The driver's N>1 code path on RCCL itself: bench.py under torchrun with
     the default backend ("nccl" = RCCL) at world size 1 (CYAES_BENCH_FORCE_DIST
