@@ -49,6 +49,9 @@
 #ifndef CYAES_RAGGED_PRIO_LATE
 #define CYAES_RAGGED_PRIO_LATE 1  // ragged decrypt: progress atomic after the step's loads
 #endif
+#ifndef CYAES_ENC_NEXT_PREFETCH
+#define CYAES_ENC_NEXT_PREFETCH 0  // uniform lane encrypt: prefetch the lane's next payload (A/B)
+#endif
 #ifndef CYAES_RAGGED_ALIGNED_STORES
 #define CYAES_RAGGED_ALIGNED_STORES 0  // ragged lane encrypt: 16-B aligned window stores (A/B)
 #endif
@@ -448,6 +451,12 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     const uint64_t wstride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t wbase0 = (uint64_t)blockIdx.x * blockDim.x + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
 
+#if CYAES_ENC_NEXT_PREFETCH
+    // Uniform batches (A/B): the lane's next payload (p + wstride) has its first
+    // chunk loaded during this payload's last chunk or tail, and carried here.
+    uint4 nxt[8];
+    bool have_nxt = false;
+#endif
     for (uint64_t wbase = wbase0; wbase < a.npayloads; wbase += wstride) {
         const uint64_t p = wbase + lane;
         const bool active = p < a.npayloads;
@@ -480,10 +489,21 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
 #endif
                 uint32_t i = 0;
                 uint4 b[8];
+#if CYAES_ENC_NEXT_PREFETCH
+                const bool nx_ok = !RAGGED && nb >= 8 && p + wstride < a.npayloads;
+                const uint8_t* const nsrc0 = a.in + (p + wstride) * (uint64_t)a.payload_bytes;
+                if (nb >= 8 && !RAGGED && have_nxt) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) b[j] = nxt[j];
+                } else
+#endif
                 if (nb >= 8) {
 #pragma unroll
                     for (int j = 0; j < 8; j++) b[j] = ldb<RAGGED>(src, j);
                 }
+#if CYAES_ENC_NEXT_PREFETCH
+                have_nxt = false;
+#endif
                 bool have_tail = false;  // b[0, nb - i) already hold the last partial chunk
                 for (; i + 8 <= nb; i += 8) {
                     const bool more = i + 16 <= nb;
@@ -501,6 +521,12 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
 #pragma unroll
                         for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(nsrc, j);
                     }
+#if CYAES_ENC_NEXT_PREFETCH
+                    else if (nx_ok) {  // last chunk, no tail: the next payload's first chunk
+#pragma unroll
+                        for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(nsrc0, j);
+                    }
+#endif
 #else
                     if (more) {
 #pragma unroll
@@ -547,6 +573,13 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
 #pragma unroll
                         for (int j = 0; j < 8; j++) b[j] = bn[j];
                     }
+#if CYAES_ENC_NEXT_PREFETCH
+                    else if (nx_ok) {
+#pragma unroll
+                        for (int j = 0; j < 8; j++) nxt[j] = bn[j];
+                        have_nxt = true;
+                    }
+#endif
                     have_tail = tail;
 #endif
                 }
@@ -559,6 +592,13 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                             for (int j = 0; j < 7; j++) b[j] = b[j + 1];
                         }
                     }
+                }
+#endif
+#if CYAES_ENC_NEXT_PREFETCH
+                if (nx_ok && i < nb) {  // a tail follows: the next payload's first chunk loads during it
+#pragma unroll
+                    for (int j = 0; j < 8; j++) nxt[j] = ldb<RAGGED>(nsrc0, j);
+                    have_nxt = true;
                 }
 #endif
                 for (; i < nb; i++) {  // partial last chunk: from b (prefetched) or loaded here
