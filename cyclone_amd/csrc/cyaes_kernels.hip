@@ -24,9 +24,12 @@
 //    a per-payload key index is handled by a waterfall over the distinct keys
 //    present in a wave, normally one).
 //  * Encrypt (serial CBC): one lane = one payload chain, 8 blocks (128 B, one
-//    full line per lane) loaded per step (k_encrypt).  Batches with too few
-//    chains to fill the chip, and ragged ones, use four lanes per chain, one
-//    state word each, exchanging lookups by DPP quad_perm (k_encrypt_quad).
+//    full line per lane) loaded per step, the next step's 8 loads in flight
+//    during this step's rounds through one load path (a partial last step
+//    loads the payload's last 8 blocks), so a step never waits for the
+//    previous step's stores (k_encrypt).  Batches with too few chains to fill
+//    the chip (uniform or ragged) use four lanes per chain, one state word
+//    each, exchanging lookups by DPP quad_perm (k_encrypt_quad).
 //  * Decrypt (block-parallel): one lane = one 16-B block, four rows decrypted
 //    together, each wave-instruction loads 1 KiB contiguous; the previous
 //    ciphertext block comes from the neighbour lane (DPP wave_shr:1), the
