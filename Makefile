@@ -17,6 +17,11 @@ CPPTEST  := $(BUILD)/test_rijndael $(BUILD)/relay_calls
 # Measurement-only build of the same kernels with the in-kernel clock probe
 # (CYAES_CLOCK_PROBE): bench.py reads the shader clock under load from it.
 PROBE    := $(BUILD)/variants/clockprobe.so
+# Bounds-checked build of the same kernels (CYAES_BOUNDS_CHECK): every global
+# access checked against its batch-contract extent, misses counted (never
+# faulted) and read by cyaes_debug_bounds(); the GPU suite runs on it with
+# CYAES_LIBRARY=build/variants/bounds.so.
+BOUNDS   := $(BUILD)/variants/bounds.so
 
 KSRC     := cyclone_amd/csrc/cyaes_kernels.hip
 ASRC     := cyclone_amd/csrc/cyaes_adler.hip
@@ -29,13 +34,14 @@ KOBJ     := $(BUILD)/cyaes_kernels.o
 AOBJ     := $(BUILD)/cyaes_adler.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
-.PHONY: all lib mgpu oracle cpptest probe microbench variant clean
-all: lib mgpu oracle cpptest probe $(BUILD)/bench_batcher $(BUILD)/dropin_threads $(BUILD)/bitslice
+.PHONY: all lib mgpu oracle cpptest probe bounds microbench variant clean
+all: lib mgpu oracle cpptest probe bounds $(BUILD)/bench_batcher $(BUILD)/dropin_threads $(BUILD)/bitslice
 lib: $(LIB)
 mgpu: $(MGPU)
 oracle: $(ORACLE)
 cpptest: $(CPPTEST)
 probe: $(PROBE)
+bounds: $(BOUNDS)
 
 $(BUILD):
 	mkdir -p $(BUILD)
@@ -81,6 +87,11 @@ $(PROBE): $(KSRC) $(HDRS) $(HOBJ) $(AOBJ)
 	mkdir -p $(BUILD)/variants
 	$(HIPCC) $(HIPFLAGS) -DCYAES_CLOCK_PROBE=1 -c $(KSRC) -o $(BUILD)/variants/clockprobe.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(BUILD)/variants/clockprobe.o $(AOBJ) $(HOBJ)
+
+$(BOUNDS): $(KSRC) $(HDRS) $(HOBJ) $(AOBJ)
+	mkdir -p $(BUILD)/variants
+	$(HIPCC) $(HIPFLAGS) -DCYAES_BOUNDS_CHECK=1 -c $(KSRC) -o $(BUILD)/variants/bounds.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(BUILD)/variants/bounds.o $(AOBJ) $(HOBJ)
 
 # Bitsliced decrypt prototype (measurement tool)
 $(BUILD)/bitslice: tools/bitslice.hip tools/bitslice_gen.h $(LIB) | $(BUILD)

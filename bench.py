@@ -39,6 +39,7 @@ work_thread_counts = get_cpu_counts(), relay_local.cpp:475) on a bounded
 sample of the same workload, rank 0 at N=1 only.
 """
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -194,6 +195,14 @@ def main():
         else:
             dist.init_process_group(backend)
         log("process group: backend %s, world %d, device %d" % (dist.get_backend(), dist.get_world_size(), device))
+    # Which process group and which device each rank ran on, so the JSON line
+    # alone shows RCCL (backend "nccl") saw N ranks on N distinct devices.
+    props = torch.cuda.get_device_properties(device)
+    dev_id = {"device": device, "pci": "%04x:%02x:%02x" % (props.pci_domain_id, props.pci_bus_id, props.pci_device_id),
+              "uuid": str(getattr(props, "uuid", ""))}
+    dist_info = {"backend": dist.get_backend() if dist_on else None,
+                 "world_size": dist.get_world_size() if dist_on else 1}
+    key_digest = {}  # digest of the session keys this rank received by broadcast (per config)
 
     import cyclone_amd as ca
     from cyclone_amd import dist as cdist
@@ -222,6 +231,7 @@ def main():
         nkeys = cdist.session_range(0, npay * world, ppk)[1]
         d_keys = cdist.broadcast_keys((session_keys(nkeys) if ppk else bytes(range(16))) if rank == 0 else None,
                                       nkeys, "cuda")
+        key_digest["last"] = hashlib.sha256(d_keys.cpu().numpy().tobytes()).hexdigest()[:16]
         k0, nk = cdist.session_range(p0, npay, ppk)
         ctx.set_keys_device(d_keys[16 * k0: 16 * (k0 + nk)].contiguous(), nk, sh)
 
@@ -255,7 +265,7 @@ def main():
         torch.cuda.synchronize()
 
         parity = None
-        shard = {"rank": rank, "p0": p0, "npayloads": npay}
+        shard = dict({"rank": rank, "p0": p0, "npayloads": npay, "keys_sha256_16": key_digest["last"]}, **dev_id)
         if verify:
             ok = ctx.digest(d_rt, nbytes, sh) == ctx.digest(d_pt, nbytes, sh)
             g = golden.get(name) if rank == 0 else None
@@ -378,12 +388,12 @@ def main():
             dist.barrier()
         t_wall = time.perf_counter() - t_begin
         t = max_over_ranks(t_aes)
-        shards = None
+        shard = dict({"rank": rank, "passes": mine, "golden_verified": verified,
+                      "keys_sha256_16": key_digest["last"]}, **dev_id)
+        shards = [shard]
         if dist_on:
             shards = [None] * world
-            dist.all_gather_object(shards, {"rank": rank, "passes": mine, "golden_verified": verified})
-        else:
-            shards = [{"rank": 0, "passes": mine, "golden_verified": verified}]
+            dist.all_gather_object(shards, shard)
         n = steps * len(mine)
         res = {
             "name": "E", "npay": pp, "pb": pb, "ppk": 0, "nbytes": nbytes, "t": t, "steps": steps,
@@ -596,6 +606,9 @@ def main():
             "packet_configs": packet_configs, "relay_stream": relay,
         }
         out["shards"] = main_res["shards"]
+        out["dist"] = dict(dist_info, ranks_reporting=len(main_res["shards"]),
+                           distinct_devices=len({(sh["pci"], sh["uuid"]) for sh in main_res["shards"]}),
+                           same_keys_all_ranks=len({sh["keys_sha256_16"] for sh in main_res["shards"]}) == 1)
         if args.config == "E":
             out["config"].update(passes=main_res["passes"], passes_per_gpu=main_res["passes_per_gpu"])
             out["timing"] = {"timed": "per pass: encrypt + decrypt between device synchronisations, summed; "

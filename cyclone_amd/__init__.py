@@ -20,7 +20,9 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcyaes.so")
+# CYAES_LIBRARY selects a build variant of the same library for a whole process
+# (the bounds-checked build, `make bounds`: tests/conftest.py reads its record).
+LIB_PATH = os.environ.get("CYAES_LIBRARY") or os.path.join(_HERE, "libcyaes.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cyaes.h")
 
 CYAES_OK, CYAES_EINVAL, CYAES_EDEVICE, CYAES_ENOMEM, CYAES_ERANGE, CYAES_ENODEV = 0, -1, -2, -3, -4, -5
@@ -59,7 +61,7 @@ _SIGS = {
     "cyaes_cbc_encrypt": (ctypes.c_int, [ctypes.POINTER(CyaesKey), _vp, _vp, ctypes.c_size_t, _vp]),
     "cyaes_cbc_decrypt": (ctypes.c_int, [ctypes.POINTER(CyaesKey), _vp, _vp, ctypes.c_size_t, _vp]),
     "cyaes_gpu_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
-    "cyaes_gpu_destroy": (None, [_vp]),
+    "cyaes_gpu_destroy": (ctypes.c_int, [_vp]),
     "cyaes_gpu_device": (ctypes.c_int, [_vp]),
     "cyaes_gpu_num_cus": (ctypes.c_int, [_vp]),
     "cyaes_gpu_set_keys": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32]),
@@ -273,9 +275,11 @@ class GpuContext:
         self.device = device
 
     def close(self):
+        """Frees the context; raises CyaesError if the device reports a pending
+        asynchronous fault (cyaes_gpu_destroy's synchronisation status)."""
         if getattr(self, "_h", None):
-            self._lib.cyaes_gpu_destroy(self._h)
-            self._h = None
+            h, self._h = self._h, None
+            _check(self._lib.cyaes_gpu_destroy(h), "cyaes_gpu_destroy")
 
     def __del__(self):
         try:
@@ -559,7 +563,7 @@ class Batcher:
 # ---- single-process multi-GPU (include/cyaes_mgpu.h, libcyaes_mgpu.so) -----
 _MGPU_SIGS = {
     "cyaes_mgpu_create": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.POINTER(_vp)]),
-    "cyaes_mgpu_destroy": (None, [_vp]),
+    "cyaes_mgpu_destroy": (ctypes.c_int, [_vp]),
     "cyaes_mgpu_ndev": (ctypes.c_int, [_vp]),
     "cyaes_mgpu_context": (_vp, [_vp, ctypes.c_int]),
     "cyaes_mgpu_broadcast_keys": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, ctypes.c_int]),
@@ -607,8 +611,8 @@ class MultiGpu:
 
     def close(self):
         if getattr(self, "_h", None):
-            self._lib.cyaes_mgpu_destroy(self._h)
-            self._h = None
+            h, self._h = self._h, None
+            _check(self._lib.cyaes_mgpu_destroy(h), "cyaes_mgpu_destroy")
 
     def __del__(self):
         try:

@@ -38,31 +38,15 @@
 //    batches pack groups of up to 64 payloads into the rows (k_decrypt_ragged).
 //  * Waves of a workgroup are kept level by progress-feedback priority
 //    (prio_feedback), so none runs a starved tail.
+//
+// Build variants (Makefile): CYAES_CLOCK_PROBE (bench.py's in-kernel clock)
+// and CYAES_BOUNDS_CHECK (every global access checked against the extent the
+// batch contract gives it; misses are counted, never faulted).  The rejected
+// A/B variants of rounds 1-2 are recorded in profiles/r0{1,2}/ab_*.txt.
 #include "cyaes_internal.h"
 
-#ifndef CYAES_NO_PREFETCH
-#define CYAES_NO_PREFETCH 0    // A/B only: load each encrypt chunk at its top instead of one chunk ahead
-#endif
-#ifndef CYAES_QUAD_DPP_XOR
-#define CYAES_QUAD_DPP_XOR 0
-#endif
-#ifndef CYAES_RAGGED_REGULAR
-#define CYAES_RAGGED_REGULAR 1  // ragged decrypt: strided equal-size payload groups walk positions per lane
-#endif
-#ifndef CYAES_RAGGED_PRIO_LATE
-#define CYAES_RAGGED_PRIO_LATE 1  // ragged decrypt: progress atomic after the step's loads
-#endif
-#ifndef CYAES_ENC_NEXT_PREFETCH
-#define CYAES_ENC_NEXT_PREFETCH 0  // uniform lane encrypt: prefetch the lane's next payload (A/B)
-#endif
-#ifndef CYAES_RAGGED_ALIGNED_STORES
-#define CYAES_RAGGED_ALIGNED_STORES 0  // ragged lane encrypt: 16-B aligned window stores (A/B)
-#endif
-#ifndef CYAES_ENC_ONE_PREFETCH
-#define CYAES_ENC_ONE_PREFETCH 1  // encrypt: one prefetch path for full and partial next chunks (A/B: 0 = two paths)
-#endif
-#ifndef CYAES_TAIL_PREFETCH
-#define CYAES_TAIL_PREFETCH 1  // encrypt: prefetch a payload's partial last chunk with the chunk before
+#ifndef CYAES_BOUNDS_CHECK
+#define CYAES_BOUNDS_CHECK 0
 #endif
 
 namespace cyaes {
@@ -79,6 +63,74 @@ constexpr uint32_t kHalfB = 128;            // byte offset of table B inside a r
 // DefaultIV (cyr_rijndael.cpp:503-504) as little-endian dwords.
 constexpr uint32_t kIv0 = 0x03020100u, kIv1 = 0x07060504u, kIv2 = 0x0b0a0908u, kIv3 = 0x0f0e0d0cu;
 
+// ---- global accesses --------------------------------------------------------
+// Every global load and store of the AES kernels names the extent [lo, hi)
+// the batch contract allows it (the payload's bytes, the IV array, the key
+// table, ...).  In the CYAES_BOUNDS_CHECK build an access outside it is
+// counted in g_bounds (first offender's source line, offset and extent kept)
+// and redirected to a sink, so a stray access is reported by name instead of
+// faulting the device; cyaes_debug_bounds() reads the record.  In the product
+// build the extent is dead code.
+struct Ext {
+    const uint8_t* lo;
+    const uint8_t* hi;
+};
+__device__ __forceinline__ Ext ext(const void* p, uint64_t bytes) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    return Ext{b, b + bytes};
+}
+
+#if CYAES_BOUNDS_CHECK
+__device__ unsigned long long g_bounds[4];  // misses, first miss's line, its offset from lo, the extent's size
+__device__ uint4 g_bounds_sink[64];
+template <typename T>
+__device__ __forceinline__ T* bchk(T* p, Ext e, uint32_t bytes, uint32_t line) {
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(p);
+    if (e.lo && b >= e.lo && b + bytes <= e.hi) return p;
+    if (atomicAdd(&g_bounds[0], 1ull) == 0) {
+        g_bounds[1] = line;
+        g_bounds[2] = (unsigned long long)(b - e.lo);
+        g_bounds[3] = (unsigned long long)(e.hi - e.lo);
+    }
+    return reinterpret_cast<T*>(&g_bounds_sink[__lane_id()]);
+}
+#define AT(p, e, bytes) bchk((p), (e), (bytes), __LINE__)
+#else
+#define AT(p, e, bytes) ((void)(e), (p))
+#endif
+
+// 16-B block at a 4-byte-aligned address (ragged batches: relay packets put
+// the payload at packet offset 12).  Still one global_load/store_dwordx4.
+struct __attribute__((aligned(4))) Blk4 {
+    uint32_t x, y, z, w;
+};
+#define LD16(p, e) (*AT(reinterpret_cast<const uint4*>(p), (e), 16))
+#define ST16(p, e, v) (*AT(reinterpret_cast<uint4*>(p), (e), 16) = (v))
+#define LD16U(p, e) blk_in(*AT(reinterpret_cast<const Blk4*>(p), (e), 16))
+#define ST16U(p, e, v) (*AT(reinterpret_cast<Blk4*>(p), (e), 16) = blk_out(v))
+#define LD4(p, e) (*AT(reinterpret_cast<const uint32_t*>(p), (e), 4))
+#define ST4(p, e, v) (*AT(reinterpret_cast<uint32_t*>(p), (e), 4) = (v))
+#define LD8(p, e) (*AT(reinterpret_cast<const uint64_t*>(p), (e), 8))
+__device__ __forceinline__ uint4 blk_in(Blk4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ Blk4 blk_out(uint4 v) { return Blk4{v.x, v.y, v.z, v.w}; }
+
+// Block i of a payload at base (extent e): 16-B aligned (U = false) or 4-B aligned (U = true).
+template <bool U>
+__device__ __forceinline__ uint4 ldb(const uint8_t* base, uint32_t i, Ext e) {
+    if (U) return LD16U(base + 16ull * i, e);
+    return LD16(base + 16ull * i, e);
+}
+template <bool U>
+__device__ __forceinline__ void stb(uint8_t* base, uint32_t i, uint4 v, Ext e) {
+    if (U) ST16U(base + 16ull * i, e, v);
+    else ST16(base + 16ull * i, e, v);
+}
+
+// Extents of the batch arrays every kernel shares.
+__device__ __forceinline__ Ext iv_ext(const uint8_t* iv, uint64_t npayloads) { return ext(iv, 16 * npayloads); }
+__device__ __forceinline__ Ext key_ext(const KeySel& ks) { return ext(ks.table, (uint64_t)ks.nkeys * kSchedWords * 4); }
+
+// ---- table lookups ----------------------------------------------------------
 __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_rotateleft32(x, 8); }
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -155,43 +207,17 @@ __device__ __forceinline__ uint32_t enc_last(const char* lds, uint32_t lo, uint3
     return merge4(l0, l1, l2, l3);
 }
 
-#if CYAES_VALU_FILLER
-// Experiment only (make variant DEFS=-DCYAES_VALU_FILLER=N): N extra full-rate
-// VALU ops per round in 4 independent chains, to measure how much idle VALU
-// issue the LDS-bound rounds leave (and what it costs in clock).
-struct Filler {
-    uint32_t a[4] = {1, 2, 3, 4};
-    __device__ __forceinline__ void run(uint32_t x, uint32_t y) {
-#pragma unroll
-        for (int i = 0; i < CYAES_VALU_FILLER; i++)
-            asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[i & 3]) : "v"(x), "v"(y));
-    }
-    __device__ __forceinline__ uint32_t sum() const { return a[0] ^ a[1] ^ a[2] ^ a[3]; }
-};
-__device__ Filler* g_filler_sink;
-#define FILLER_RUN(x, y) filler.run(x, y)
-#else
-#define FILLER_RUN(x, y)
-#endif
-
 // s = plaintext ^ chain ^ ek[0..3] on entry, ciphertext on exit.
 __device__ __forceinline__ void enc_block(const char* lds, uint32_t lo, const uint32_t* __restrict__ ek,
                                           uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
-#if CYAES_VALU_FILLER
-    Filler filler;
-#endif
 #pragma unroll
     for (int r = 1; r < 10; r++) {
         const uint32_t a0 = tcol(lds, lo, s0, s1, s2, s3, ek[4 * r + 0]);
         const uint32_t a1 = tcol(lds, lo, s1, s2, s3, s0, ek[4 * r + 1]);
         const uint32_t a2 = tcol(lds, lo, s2, s3, s0, s1, ek[4 * r + 2]);
         const uint32_t a3 = tcol(lds, lo, s3, s0, s1, s2, ek[4 * r + 3]);
-        FILLER_RUN(s0, s2);
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     }
-#if CYAES_VALU_FILLER
-    if (filler.sum() == 0x9E3779B9u && lo == 0xFFFFFFFFu) g_filler_sink->a[0] = 1;  // never true: keeps the work
-#endif
     const uint32_t o0 = enc_last(lds, lo, s0, s1, s2, s3) ^ ek[40];
     const uint32_t o1 = enc_last(lds, lo, s1, s2, s3, s0) ^ ek[41];
     const uint32_t o2 = enc_last(lds, lo, s2, s3, s0, s1) ^ ek[42];
@@ -280,9 +306,11 @@ __device__ __forceinline__ void dec_cbc(const char* lds, uint32_t lo, const uint
 }
 
 // Key index of payload p (cyaes.h): key_idx[p] | p / ppk | 0, clamped.
-__device__ __forceinline__ uint32_t key_index(const KeySel& ks, uint64_t p, bool active, uint32_t* status) {
+__device__ __forceinline__ uint32_t key_index(const KeySel& ks, uint64_t p, uint64_t npayloads, bool active,
+                                              uint32_t* status) {
     if (!active) return 0;
-    uint32_t kid = ks.key_idx ? ks.key_idx[p] : (ks.ppk.d ? fastdiv((uint32_t)p, ks.ppk) : 0u);
+    uint32_t kid = ks.key_idx ? LD4(ks.key_idx + p, ext(ks.key_idx, 4 * npayloads))
+                              : (ks.ppk.d ? fastdiv((uint32_t)p, ks.ppk) : 0u);
     if (kid >= ks.nkeys) {
         atomicOr(status, 1u);
         kid = ks.nkeys - 1;
@@ -292,23 +320,21 @@ __device__ __forceinline__ uint32_t key_index(const KeySel& ks, uint64_t p, bool
 
 __device__ __forceinline__ uint32_t rl63(uint32_t v) { return __builtin_amdgcn_readlane(v, 63); }
 
-// Loads one 44-word half of a key schedule (wave-uniform address) into SGPRs.
-// The table is only read by the kernels, but the compiler cannot prove the
-// batch's stores do not alias it, so it would otherwise keep the words in
-// VGPRs or re-load them with vector loads inside the block loop.
-__device__ __forceinline__ void load_sched(const uint32_t* p, uint32_t (&k)[44]) {
-    const uint4* p4 = reinterpret_cast<const uint4*>(p);
+// Loads one 44-word half of schedule `kid` (half 0: ek, 1: dk; wave-uniform
+// address) into SGPRs.  The table is only read by the kernels, but the
+// compiler cannot prove the batch's stores do not alias it, so it would
+// otherwise keep the words in VGPRs or re-load them with vector loads inside
+// the block loop.
+__device__ __forceinline__ void load_sched(const KeySel& ks, uint32_t kid, int half, uint32_t (&k)[44]) {
+    const uint32_t* p = ks.table + (uint64_t)kid * kSchedWords + 44 * half;
+    const Ext e = key_ext(ks);
 #pragma unroll
     for (int i = 0; i < 11; i++) {
-        const uint4 v = p4[i];
-#if CYAES_KEYS_VGPR
-        k[4 * i + 0] = v.x; k[4 * i + 1] = v.y; k[4 * i + 2] = v.z; k[4 * i + 3] = v.w;
-#else
+        const uint4 v = LD16(p + 4 * i, e);
         k[4 * i + 0] = __builtin_amdgcn_readfirstlane(v.x);
         k[4 * i + 1] = __builtin_amdgcn_readfirstlane(v.y);
         k[4 * i + 2] = __builtin_amdgcn_readfirstlane(v.z);
         k[4 * i + 3] = __builtin_amdgcn_readfirstlane(v.w);
-#endif
     }
 }
 
@@ -320,9 +346,8 @@ __device__ __forceinline__ void load_sched(const uint32_t* p, uint32_t (&k)[44])
 // wave trailing the block's leader by d steps runs at priority min(d / div, 3).
 // The waves then finish together (probe: within 1 %); -7.5 % encrypt and -8 %
 // decrypt time on config C (tools/ab.py).  Lockstepping the waves with
-// s_barrier instead was measured worse (encrypt +5 %, decrypt -4 %).  CYAES_NO_PRIO=1 builds without it.
+// s_barrier instead was measured worse (encrypt +5 %, decrypt -4 %).
 __device__ __forceinline__ void prio_feedback(uint32_t* lead, uint32_t step, uint32_t div) {
-#if !CYAES_NO_PRIO
     // first active lane publishes (lane 0 may be masked off in a waterfall)
     const uint32_t fl = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
     uint32_t m = 0;
@@ -334,83 +359,17 @@ __device__ __forceinline__ void prio_feedback(uint32_t* lead, uint32_t step, uin
     else if (d == 2) __builtin_amdgcn_s_setprio(2);
     else if (d == 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
-#endif
 }
-#ifndef CYAES_ENC_PRIO_DIV
-#define CYAES_ENC_PRIO_DIV 4
-#endif
-#ifndef CYAES_DEC_PRIO_DIV
-#define CYAES_DEC_PRIO_DIV 8
-#endif
-constexpr uint32_t kEncPrioDiv = CYAES_ENC_PRIO_DIV;  // steps = 8-block chunks (A/B: 1, 2, 4, 8 -> 4 best)
-constexpr uint32_t kDecPrioDiv = CYAES_DEC_PRIO_DIV;  // steps = 64*kDecRows-block rows (A/B: 4, 8, 16 -> 8)
-
-
-// 16-B block at a 4-byte-aligned address (ragged batches: relay packets put
-// the payload at packet offset 12).  Still one global_load/store_dwordx4.
-struct __attribute__((aligned(4))) Blk4 {
-    uint32_t x, y, z, w;
-};
-__device__ __forceinline__ uint4 ldu(const uint8_t* p) {
-    const Blk4 v = *reinterpret_cast<const Blk4*>(p);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void stu(uint8_t* p, uint4 v) { *reinterpret_cast<Blk4*>(p) = Blk4{v.x, v.y, v.z, v.w}; }
-// Block i of a payload: 16-B aligned (U = false) or 4-B aligned (U = true).
-// (Measured on a stream of 1 M relay packets, lane kernel, profiles/r02/ab_ragged_stores.txt:
-// 16-B stores at 4-B aligned addresses cost ~0.3 ms of 1.75; the loads ~0.02.
-// Four dword stores instead: 2.54 ms; rotating each step's words into aligned
-// 16-B slots: 2.03 ms (the rotation's registers spill).  The cost probes below
-// stay for A/B builds.)
-template <bool U>
-__device__ __forceinline__ uint4 ldb(const uint8_t* base, uint32_t i) {
-#if CYAES_PROBE_ALIGNED_LOADS  // cost probe only (wrong output): ragged loads from the 16-B aligned address
-    if (U) return *reinterpret_cast<const uint4*>((uintptr_t)(base + 16ull * i) & ~(uintptr_t)15);
-#endif
-    if (U) return ldu(base + 16ull * i);
-    return reinterpret_cast<const uint4*>(base)[i];
-}
-template <bool U>
-__device__ __forceinline__ void stb(uint8_t* base, uint32_t i, uint4 v) {
-#if CYAES_PROBE_ALIGNED_STORES  // cost probe only (wrong output): ragged stores to the 16-B aligned address
-    if (U) {
-        *reinterpret_cast<uint4*>((uintptr_t)(base + 16ull * i) & ~(uintptr_t)15) = v;
-        return;
-    }
-#endif
-    if (U) stu(base + 16ull * i, v);
-    else reinterpret_cast<uint4*>(base)[i] = v;
-}
-
-#if CYAES_RAGGED_ALIGNED_STORES
-// Ragged encrypt, 4-B aligned payloads (A/B): store 16-B aligned windows
-// instead of 4-B aligned blocks.  With the payload mis words past a 16-B
-// boundary, window k holds the last mis words of block k-1 and the first
-// 4 - mis words of block k: S = prev | cur (8 words), window = S[4-mis, 8-mis),
-// picked in two select stages (shift by 1 word, then by 2).
-__device__ __forceinline__ uint4 awin(uint4 prev, uint4 cur, uint32_t mis) {
-    const bool s1 = mis & 1u, s2 = mis & 2u;
-    const uint32_t t2 = s1 ? prev.y : prev.z, t3 = s1 ? prev.z : prev.w, t4 = s1 ? prev.w : cur.x;
-    const uint32_t t5 = s1 ? cur.x : cur.y, t6 = s1 ? cur.y : cur.z, t7 = s1 ? cur.z : cur.w;
-    return make_uint4(s2 ? t2 : t4, s2 ? t3 : t5, s2 ? t4 : t6, s2 ? t5 : t7);
-}
-// Words [from, to) of window w at the 16-B aligned p (the payload's first and last windows).
-__device__ __forceinline__ void awin_part(uint8_t* p, uint4 w, uint32_t from, uint32_t to) {
-    uint32_t* q = reinterpret_cast<uint32_t*>(p);
-    if (from <= 0 && 0 < to) q[0] = w.x;
-    if (from <= 1 && 1 < to) q[1] = w.y;
-    if (from <= 2 && 2 < to) q[2] = w.z;
-    if (from <= 3 && 3 < to) q[3] = w.w;
-}
-#endif
+constexpr uint32_t kEncPrioDiv = 4;  // steps = 8-block chunks (A/B: 1, 2, 4, 8 -> 4 best)
+constexpr uint32_t kDecPrioDiv = 8;  // steps = 64*kDecRows-block rows (A/B: 4, 8, 16 -> 8)
 
 __device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kIv2, kIv3); }
 
 #if CYAES_CLOCK_PROBE
-// Variant builds only (make variant DEFS=-DCYAES_CLOCK_PROBE=1): per-wave
-// shader cycles (s_memtime) and wall ticks (s_memrealtime, 100 MHz per
-// tools/clockcal.hip) over the kernel body, summed per kernel kind into
-// g_probe and read by cyaes_debug_probe() (tools/ab.py prints the clock).
+// Variant builds only (make probe): per-wave shader cycles (s_memtime) and
+// wall ticks (s_memrealtime, 100 MHz per tools/clockcal.hip) over the kernel
+// body, summed per kernel kind into g_probe and read by cyaes_debug_probe()
+// (bench.py and tools/ab.py print the clock).
 __device__ unsigned long long g_probe[2][4];  // [enc, dec] x {cycles, ticks, waves, max ticks}
 struct ClockProbe {
     uint64_t t0, r0;
@@ -450,29 +409,24 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
     // Block size: kEncThreads for big batches; fewer for small ones, so that
-    // few chains spread over many CUs (cyaes_runtime.cpp, small_grid).
+    // few chains spread over many CUs (cyaes_runtime.cpp, wave_shape).
     const uint64_t wstride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t wbase0 = (uint64_t)blockIdx.x * blockDim.x + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+    const Ext iv_in_e = iv_ext(a.iv_in, a.npayloads), iv_out_e = iv_ext(a.iv_out, a.npayloads);
 
-#if CYAES_ENC_NEXT_PREFETCH
-    // Uniform batches (A/B): the lane's next payload (p + wstride) has its first
-    // chunk loaded during this payload's last chunk or tail, and carried here.
-    uint4 nxt[8];
-    bool have_nxt = false;
-#endif
     for (uint64_t wbase = wbase0; wbase < a.npayloads; wbase += wstride) {
         const uint64_t p = wbase + lane;
         const bool active = p < a.npayloads;
         uint64_t off;
         uint32_t nb;
         if (RAGGED) {
-            off = active ? a.offsets[p] : 0;
-            nb = active ? (a.nbytes[p] >> 4) : 0;
+            off = active ? LD8(a.offsets + p, ext(a.offsets, 8 * a.npayloads)) : 0;
+            nb = active ? (LD4(a.nbytes + p, ext(a.nbytes, 4 * a.npayloads)) >> 4) : 0;
         } else {
             off = p * (uint64_t)a.payload_bytes;
             nb = active ? (a.payload_bytes >> 4) : 0;
         }
-        const uint32_t kid = KEYED ? key_index(a.keys, p, active, a.status) : 0u;
+        const uint32_t kid = KEYED ? key_index(a.keys, p, a.npayloads, active, a.status) : 0u;
         bool pending = active;
         while (true) {  // waterfall over the distinct keys of this wave
             const uint64_t m = __ballot(pending);
@@ -481,66 +435,34 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
             if (pending && (!KEYED || kid == ku)) {
                 pending = false;
                 uint32_t ek[44];
-                load_sched(a.keys.table + (uint64_t)ku * kSchedWords, ek);
-                uint4 c = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
+                load_sched(a.keys, ku, 0, ek);
+                uint4 c = a.iv_in ? LD16(a.iv_in + 16 * p, iv_in_e) : default_iv();
                 const uint8_t* src = a.in + off;  // ragged: 4-B aligned
                 uint8_t* dst = a.out + off;
-#if CYAES_RAGGED_ALIGNED_STORES
-                const uint32_t mis = RAGGED ? (uint32_t)(((uintptr_t)dst & 15u) >> 2) : 0u;
-                uint8_t* const adst = dst - 4u * mis;  // 16-B aligned
-                uint4 carry = make_uint4(0, 0, 0, 0);  // the previous block (its last mis words go out with the next)
-#endif
+                const Ext se = ext(src, 16ull * nb), de = ext(dst, 16ull * nb);  // this payload's bytes
                 uint32_t i = 0;
                 uint4 b[8];
-#if CYAES_ENC_NEXT_PREFETCH
-                const bool nx_ok = !RAGGED && nb >= 8 && p + wstride < a.npayloads;
-                const uint8_t* const nsrc0 = a.in + (p + wstride) * (uint64_t)a.payload_bytes;
-                if (nb >= 8 && !RAGGED && have_nxt) {
-#pragma unroll
-                    for (int j = 0; j < 8; j++) b[j] = nxt[j];
-                } else
-#endif
                 if (nb >= 8) {
 #pragma unroll
-                    for (int j = 0; j < 8; j++) b[j] = ldb<RAGGED>(src, j);
+                    for (int j = 0; j < 8; j++) b[j] = ldb<RAGGED>(src, j, se);
                 }
-#if CYAES_ENC_NEXT_PREFETCH
-                have_nxt = false;
-#endif
-                bool have_tail = false;  // b[0, nb - i) already hold the last partial chunk
+                bool have_tail = false;  // b[8 - (nb - i), 8) already hold the last partial chunk
                 for (; i + 8 <= nb; i += 8) {
                     const bool more = i + 16 <= nb;
-                    const bool tail = CYAES_TAIL_PREFETCH && !CYAES_NO_PREFETCH && !more && i + 8 < nb;  // partial last chunk
-#if !CYAES_NO_PREFETCH  // A/B: -8% encrypt time vs loading at the top of the chunk
-                    uint4 bn[8];  // next chunk's loads in flight during this chunk's rounds
-#if CYAES_ENC_ONE_PREFETCH
+                    const bool tail = !more && i + 8 < nb;  // partial last chunk
+                    // Next chunk's loads in flight during this chunk's rounds (-8 %
+                    // encrypt time).  One set of 8 loads for both cases: a partial
+                    // last chunk loads the payload's last 8 blocks (its tail then
+                    // sits at the top of bn).  With every bn[j] defined on this
+                    // path the compiler no longer waits for this chunk's stores
+                    // (s_waitcnt vmcnt(0)) before the next chunk's loads; it waits
+                    // only for the loads (profiles/r02/ab_onepf.txt).
+                    uint4 bn[8];
                     if (more || tail) {
-                        // One set of 8 loads for both cases: a partial last chunk loads
-                        // the payload's last 8 blocks (its tail then sits at the top of
-                        // bn).  With every bn[j] defined on this path the compiler no
-                        // longer waits for this chunk's stores (s_waitcnt vmcnt(0))
-                        // before the next chunk's loads; it waits only for the loads.
                         const uint8_t* nsrc = src + 16ull * (more ? i + 8 : nb - 8);
 #pragma unroll
-                        for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(nsrc, j);
+                        for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(nsrc, j, se);
                     }
-#if CYAES_ENC_NEXT_PREFETCH
-                    else if (nx_ok) {  // last chunk, no tail: the next payload's first chunk
-#pragma unroll
-                        for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(nsrc0, j);
-                    }
-#endif
-#else
-                    if (more) {
-#pragma unroll
-                        for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(src, i + 8 + j);
-                    } else if (tail) {
-#pragma unroll
-                        for (int j = 0; j < 7; j++)
-                            if (i + 8 + j < nb) bn[j] = ldb<RAGGED>(src, i + 8 + j);
-                    }
-#endif
-#endif
                     prio_feedback(&lead, ++prog, kEncPrioDiv);
 #pragma unroll
                     for (int j = 0; j < 8; j++) {
@@ -550,43 +472,15 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                         c = make_uint4(s0, s1, s2, s3);
                         b[j] = c;
                     }
-#if CYAES_RAGGED_ALIGNED_STORES
-                    if (RAGGED) {
-                        uint8_t* const ac = adst + 16ull * i;
-                        const uint4 w0 = awin(carry, b[0], mis);
-                        if (i == 0) awin_part(ac, w0, mis, 4);
-                        else *reinterpret_cast<uint4*>(ac) = w0;
-#pragma unroll
-                        for (int j = 1; j < 8; j++) *reinterpret_cast<uint4*>(ac + 16 * j) = awin(b[j - 1], b[j], mis);
-                        carry = b[7];
-                    } else
-#endif
-                    {
                     uint8_t* const dchunk = dst + 16ull * i;  // one address, immediate offsets (ragged too)
 #pragma unroll
-                    for (int j = 0; j < 8; j++) stb<RAGGED>(dchunk, j, b[j]);  // (nt stores measured 3.6x slower)
-                    }
-#if CYAES_NO_PREFETCH
-                    if (more) {
-#pragma unroll
-                        for (int j = 0; j < 8; j++) b[j] = ldb<RAGGED>(src, i + 8 + j);
-                    }
-#else
+                    for (int j = 0; j < 8; j++) stb<RAGGED>(dchunk, j, b[j], de);  // (nt stores measured 3.6x slower)
                     if (more || tail) {
 #pragma unroll
                         for (int j = 0; j < 8; j++) b[j] = bn[j];
                     }
-#if CYAES_ENC_NEXT_PREFETCH
-                    else if (nx_ok) {
-#pragma unroll
-                        for (int j = 0; j < 8; j++) nxt[j] = bn[j];
-                        have_nxt = true;
-                    }
-#endif
                     have_tail = tail;
-#endif
                 }
-#if CYAES_ENC_ONE_PREFETCH
                 if (have_tail) {  // the tail's nb - i blocks sit in b[8 - (nb - i), 8): move them down to b[0]
 #pragma unroll
                     for (int sft = 1; sft < 8; sft++) {
@@ -596,43 +490,21 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                         }
                     }
                 }
-#endif
-#if CYAES_ENC_NEXT_PREFETCH
-                if (nx_ok && i < nb) {  // a tail follows: the next payload's first chunk loads during it
-#pragma unroll
-                    for (int j = 0; j < 8; j++) nxt[j] = ldb<RAGGED>(nsrc0, j);
-                    have_nxt = true;
-                }
-#endif
                 for (; i < nb; i++) {  // partial last chunk: from b (prefetched) or loaded here
-                    const uint4 v = have_tail ? b[0] : ldb<RAGGED>(src, i);
+                    const uint4 v = have_tail ? b[0] : ldb<RAGGED>(src, i, se);
 #pragma unroll
                     for (int j = 0; j < 7; j++) b[j] = b[j + 1];
                     uint32_t s0 = xor3(c.x, v.x, ek[0]), s1 = xor3(c.y, v.y, ek[1]);
                     uint32_t s2 = xor3(c.z, v.z, ek[2]), s3 = xor3(c.w, v.w, ek[3]);
                     enc_block(lds, lo, ek, s0, s1, s2, s3);
                     c = make_uint4(s0, s1, s2, s3);
-#if CYAES_RAGGED_ALIGNED_STORES
-                    if (RAGGED) {
-                        const uint4 w = awin(carry, c, mis);
-                        if (i == 0) awin_part(adst, w, mis, 4);
-                        else *reinterpret_cast<uint4*>(adst + 16ull * i) = w;
-                        carry = c;
-                        continue;
-                    }
-#endif
-                    stb<RAGGED>(dst, i, c);
+                    stb<RAGGED>(dst, i, c, de);
                 }
-#if CYAES_RAGGED_ALIGNED_STORES
-                if (RAGGED && nb > 0 && mis > 0) awin_part(adst + 16ull * nb, awin(carry, carry, mis), 0, mis);
-#endif
-                if (a.iv_out) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c;
+                if (a.iv_out) ST16(a.iv_out + 16 * p, iv_out_e, c);
             }
         }
     }
 }
-
-
 
 // ---- CBC encrypt, latency-bound batches: four lanes per payload chain ------
 // A lane per chain (k_encrypt) fills the chip only with >= 16 waves of chains
@@ -649,7 +521,7 @@ constexpr uint32_t kQuadFrom2 = 0x4E;  // [2,3,0,1]
 constexpr uint32_t kQuadFrom3 = 0x93;  // [3,0,1,2]
 template <uint32_t CTRL>
 __device__ __forceinline__ uint32_t qperm(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, CYAES_QUAD_DPP_XOR ? true : false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
 }
 
 // One AES block on a quad: s = word q of (plaintext ^ chain ^ k0) in, word q of the ciphertext out.
@@ -660,12 +532,7 @@ __device__ __forceinline__ uint32_t enc_block_quad(const char* lds, uint32_t lo,
         const uint32_t a1 = ld(lds, addr1(s, lo));                          // T2[b1(s_q)] -> column q-1
         const uint32_t a2 = ld(lds + kHalfB, addr(s, lo, kSel2));           // T3[b2(s_q)] -> column q-2
         const uint32_t a3 = ld(lds + kHalfB, addr(s, lo, region1(kSel3)));  // T4[b3(s_q)] -> column q-3
-#if CYAES_QUAD_DPP_XOR
-        // two-input XORs, so the DPP moves can fold into v_xor_b32's source (VOP2 DPP)
-        s = a0 ^ (qperm<kQuadFrom1>(a1) ^ (qperm<kQuadFrom2>(a2) ^ (qperm<kQuadFrom3>(a3) ^ k[r])));
-#else
         s = xor3(a0, qperm<kQuadFrom1>(a1), xor3(qperm<kQuadFrom2>(a2), qperm<kQuadFrom3>(a3), k[r]));
-#endif
     }
     const uint32_t l0 = ld(lds + kHalfB, addr(s, lo, kSel0));   // S in byte 0 (TL3)
     const uint32_t l1 = ld(lds + kHalfB, addr1(s, lo));         // byte 1 (TL4)
@@ -688,6 +555,8 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_quad(EncArgs a) {
     const uint32_t q = threadIdx.x & 3u;
     const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
     const uint64_t nquads = (uint64_t)gridDim.x * (blockDim.x / 4);
+    const Ext iv_in_e = iv_ext(a.iv_in, a.npayloads), iv_out_e = iv_ext(a.iv_out, a.npayloads);
+    const Ext key_e = key_ext(a.keys);
     // Every lane of a wave runs the loop the same number of times (the bound
     // is per wave), so a quad never waits in a branch its partners skipped.
     const uint64_t wq0 = (uint64_t)blockIdx.x * (blockDim.x / 4) + __builtin_amdgcn_readfirstlane(threadIdx.x / 4 & ~15u);
@@ -697,21 +566,22 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_quad(EncArgs a) {
         uint64_t off;
         uint32_t nb;
         if (RAGGED) {
-            off = a.offsets[p];
-            nb = a.nbytes[p] >> 4;
+            off = LD8(a.offsets + p, ext(a.offsets, 8 * a.npayloads));
+            nb = LD4(a.nbytes + p, ext(a.nbytes, 4 * a.npayloads)) >> 4;
         } else {
             off = p * (uint64_t)a.payload_bytes;
             nb = a.payload_bytes >> 4;
         }
-        const uint32_t kid = KEYED ? key_index(a.keys, p, true, a.status) : 0u;
+        const uint32_t kid = KEYED ? key_index(a.keys, p, a.npayloads, true, a.status) : 0u;
         uint32_t k[11];
         const uint32_t* sched = a.keys.table + (uint64_t)kid * kSchedWords + q;
 #pragma unroll
-        for (int r = 0; r < 11; r++) k[r] = sched[4 * r];
-        uint32_t c = a.iv_in ? reinterpret_cast<const uint32_t*>(a.iv_in + 16 * p)[q] : (kIv0 + 0x04040404u * q);
+        for (int r = 0; r < 11; r++) k[r] = LD4(sched + 4 * r, key_e);
+        uint32_t c = a.iv_in ? LD4(a.iv_in + 16 * p + 4 * q, iv_in_e) : (kIv0 + 0x04040404u * q);
+        const Ext se = ext(a.in + off, 16ull * nb), de = ext(a.out + off, 16ull * nb);  // this payload's bytes
         const uint8_t* src = a.in + off + 4 * q;  // word q of block i at src + 16 i
         uint8_t* dst = a.out + off + 4 * q;
-        auto ldw = [&](uint32_t i) { return *reinterpret_cast<const uint32_t*>(src + 16ull * i); };
+        auto ldw = [&](uint32_t i) { return LD4(src + 16ull * i, se); };
         uint32_t i = 0;
         uint32_t b[8];
         if (nb >= 8) {
@@ -732,7 +602,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_quad(EncArgs a) {
                 b[j] = c;
             }
 #pragma unroll
-            for (int j = 0; j < 8; j++) *reinterpret_cast<uint32_t*>(dst + 16ull * (i + j)) = b[j];
+            for (int j = 0; j < 8; j++) ST4(dst + 16ull * (i + j), de, b[j]);
             if (more) {
 #pragma unroll
                 for (int j = 0; j < 8; j++) b[j] = bn[j];
@@ -740,9 +610,9 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_quad(EncArgs a) {
         }
         for (; i < nb; i++) {
             c = enc_block_quad(lds, lo, k, xor3(c, ldw(i), k[0]));
-            *reinterpret_cast<uint32_t*>(dst + 16ull * i) = c;
+            ST4(dst + 16ull * i, de, c);
         }
-        if (a.iv_out) reinterpret_cast<uint32_t*>(a.iv_out + 16 * p)[q] = c;
+        if (a.iv_out) ST4(a.iv_out + 16 * p + 4 * q, iv_out_e, c);
     }
 }
 
@@ -775,9 +645,6 @@ __device__ __forceinline__ void flat_position(const DecArgs& a, FlatPos ps, uint
     }
 }
 
-// One step of R rows at block `base`.  FULL: all 64*R blocks are in range
-// (every step but possibly the batch's last), so loads and stores are
-// unguarded and use immediate offsets off one lane pointer.
 // v (lane l-1) for lanes 1..63, old for lane 0: DPP wave_shr:1.
 __device__ __forceinline__ uint32_t shr1(uint32_t v, uint32_t old) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
@@ -788,23 +655,30 @@ __device__ __forceinline__ uint4 shr1(uint4 v, uint4 old) {
 
 // Loads the R rows of the step at `base` (c); partial steps also load each
 // block's predecessor (pv), full steps take it from the neighbour lane.
+// FULL: all 64*R blocks are in range (every step but possibly the batch's
+// last), so loads are unguarded and use immediate offsets off one lane pointer.
 template <bool FULL>
 __device__ __forceinline__ void flat_load(const DecArgs& a, uint32_t lane, uint64_t base, uint64_t end,
                                           uint4 (&c)[kDecRows], uint4 (&pv)[kDecRows]) {
     constexpr int R = kDecRows;
-    const uint4* __restrict__ in = reinterpret_cast<const uint4*>(a.in);
-    const uint64_t back = lane ? 1u : 0u;  // lane 0 reads its own block (replaced by carry)
+    const Ext ie = ext(a.in, 16 * a.nblocks);
     if (FULL) {
-        const uint64_t g0 = base + lane;
+        const uint8_t* g0 = a.in + 16 * (base + lane);
 #pragma unroll
-        for (int k = 0; k < R; k++) c[k] = in[g0 + 64 * k];
+        for (int k = 0; k < R; k++) c[k] = LD16(g0 + 1024 * k, ie);
         // pv comes from the neighbour lane in flat_step (DPP), not from memory
     } else {  // last, partial step of the batch: clamp reads into range
 #pragma unroll
         for (int k = 0; k < R; k++) {
             const uint64_t g = min(base + 64 * k + lane, end - 1);
-            c[k] = in[g];
-            pv[k] = in[g - ((k == 0) ? back : 1u)];
+            c[k] = LD16(a.in + 16 * g, ie);
+            // The predecessor of block g (lane 0 of row 0 reads its own block:
+            // the carry replaces it).  Block 0 has none: a 1-block batch (end
+            // == 1) clamps every lane to g = 0, and g - 1 would read 16 B before
+            // the buffer (r02 fault hunt, VERDICT r02 "What's weak" 1).  Block
+            // 0 is a payload start, so its pv is the IV in flat_step anyway.
+            const uint64_t back = (k == 0 && lane == 0) ? 0u : 1u;
+            pv[k] = LD16(a.in + 16 * (g >= back ? g - back : 0u), ie);
         }
     }
 }
@@ -815,7 +689,8 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
                                            uint32_t (&dk0)[44], uint32_t& dk_id, const uint4 (&c)[kDecRows],
                                            uint4 (&pv)[kDecRows]) {
     constexpr int R = kDecRows;
-    uint4* out = reinterpret_cast<uint4*>(a.out);
+    const Ext oe = ext(a.out, 16 * a.nblocks);
+    const Ext iv_in_e = iv_ext(a.iv_in, a.npayloads), iv_out_e = iv_ext(a.iv_out, a.npayloads);
     if (FULL) {
         // Predecessor blocks from the neighbour lane (DPP wave_shr:1), lane 0's
         // from the row before (or the carry): no second load of C[i-1]
@@ -833,9 +708,12 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
     // Chain restarts at payload starts inside this step.
     if (BIG) {
         const uint32_t fo = ps.bpos == 0 ? 0u : a.bpp.d - ps.bpos;  // offset of the payload start, if < 64R
-        if (fo < 64u * R) {
+        // On a partial last step the "next payload" may start at or past the
+        // batch's end: then it does not exist, and iv_in[pf] would read 16 B
+        // past the IV array (VERDICT r02 "What's weak" 1).
+        if (fo < 64u * R && (FULL || base + fo < end)) {
             const uint64_t pf = ps.bp + (ps.bpos == 0 ? 0 : 1);
-            const uint4 ivv = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * pf) : default_iv();
+            const uint4 ivv = a.iv_in ? LD16(a.iv_in + 16 * pf, iv_in_e) : default_iv();
 #pragma unroll
             for (int k = 0; k < R; k++)
                 if ((fo >> 6) == (uint32_t)k && lane == (fo & 63u)) pv[k] = ivv;
@@ -848,7 +726,7 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
             flat_position<BIG>(a, ps, lane, k, r, p);
             if (r == 0) {
                 const bool valid = FULL || base + 64 * k + lane < end;
-                pv[k] = (a.iv_in && valid) ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
+                pv[k] = (a.iv_in && valid) ? LD16(a.iv_in + 16 * p, iv_in_e) : default_iv();
             }
         }
     }
@@ -858,26 +736,14 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
             uint32_t r;
             uint64_t p;
             flat_position<BIG>(a, ps, lane, k, r, p);
-            if (r == a.bpp.d - 1 && (FULL || base + 64 * k + lane < end))
-                *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+            if (r == a.bpp.d - 1 && (FULL || base + 64 * k + lane < end)) ST16(a.iv_out + 16 * p, iv_out_e, c[k]);
         }
     }
     uint4 d[R];
 #pragma unroll
     for (int k = 0; k < R; k++) d[k] = pv[k];
     if (!KEYED) {
-#if CYAES_DEC_ILP2
-#pragma unroll
-        for (int k = 0; k < R; k += 2) {  // two rows per LDS round trip
-            const uint4 cc[2] = {c[k], c[k + 1]};
-            uint4 dd[2] = {d[k], d[k + 1]};
-            dec_cbc<2>(lds, lo, dk0, cc, dd);
-            d[k] = dd[0];
-            d[k + 1] = dd[1];
-        }
-#else
         dec_cbc<R>(lds, lo, dk0, c, d);  // all R rows per LDS round trip (A/B: ~1% over 2 rows)
-#endif
     } else {
         uint32_t kid[R];
         bool valid[R];
@@ -887,7 +753,7 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
             uint64_t p;
             flat_position<BIG>(a, ps, lane, k, r, p);
             valid[k] = FULL || base + 64 * k + lane < end;
-            kid[k] = key_index(a.keys, p, valid[k], a.status);
+            kid[k] = key_index(a.keys, p, a.npayloads, valid[k], a.status);
         }
         // Sessions are contiguous runs of payloads (config D: 256 x 92 blocks),
         // so nearly every full step has one key: decrypt all R rows together
@@ -902,7 +768,7 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
             // dk0 keeps the last session's schedule (SGPRs) across steps: a
             // session spans ~92 steps in config D
             if (k0 != dk_id) {
-                load_sched(a.keys.table + (uint64_t)k0 * kSchedWords + 44, dk0);
+                load_sched(a.keys, k0, 1, dk0);
                 dk_id = k0;
             }
             dec_cbc<R>(lds, lo, dk0, c, d);
@@ -917,7 +783,7 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
                     if (pending && kid[k] == ku) {
                         pending = false;
                         uint32_t dk[44];
-                        load_sched(a.keys.table + (uint64_t)ku * kSchedWords + 44, dk);
+                        load_sched(a.keys, ku, 1, dk);
                         const uint4 cc[1] = {c[k]};
                         uint4 dd[1] = {d[k]};
                         dec_cbc<1>(lds, lo, dk, cc, dd);
@@ -928,12 +794,13 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
         }
     }
     if (FULL) {
+        uint8_t* o0 = a.out + 16 * (base + lane);
 #pragma unroll
-        for (int k = 0; k < R; k++) out[base + lane + 64 * k] = d[k];
+        for (int k = 0; k < R; k++) ST16(o0 + 1024 * k, oe, d[k]);
     } else {
 #pragma unroll
         for (int k = 0; k < R; k++)
-            if (base + 64 * k + lane < end) out[base + 64 * k + lane] = d[k];
+            if (base + 64 * k + lane < end) ST16(a.out + 16 * (base + 64 * k + lane), oe, d[k]);
     }
     return make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));  // next carry
 }
@@ -945,7 +812,6 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
 template <bool KEYED, bool BIG, bool SESS>
 __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     constexpr int R = kDecRows;
-    static_assert(R % 2 == 0, "rows are decrypted in pairs");
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
     fill_dec_image(lds_words, a.tables);
     unsigned int* leadp = &g_dec_lead[blockIdx.x % kLeadSlots];
@@ -965,7 +831,9 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     ps.bp = begin / a.bpp.d;
     ps.bpos = (uint32_t)(begin - ps.bp * a.bpp.d);
     uint4 carry = make_uint4(0, 0, 0, 0);  // C[base-1]
-    if (ps.bpos != 0) carry = a.boundary ? a.boundary[wave] : reinterpret_cast<const uint4*>(a.in)[begin - 1];
+    if (ps.bpos != 0)  // (begin >= 1 here)
+        carry = a.boundary ? LD16(a.boundary + wave, ext(a.boundary, 16ull * gridDim.x * (kDecThreads / 64)))
+                           : LD16(a.in + 16 * (begin - 1), ext(a.in, 16 * a.nblocks));
     uint32_t dk0[44];
     uint32_t dk_id = 0;  // KEYED: session whose schedule dk0 holds (~0u: none yet)
     uint32_t sess = 0;   // SESS: session of the current step; it ends at block sess_next
@@ -973,9 +841,9 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     if (SESS) {
         sess = (uint32_t)(begin / a.sess_blocks);
         sess_next = (uint64_t)(sess + 1) * a.sess_blocks;
-        load_sched(a.keys.table + (uint64_t)sess * kSchedWords + 44, dk0);
+        load_sched(a.keys, sess, 1, dk0);
     } else if (!KEYED) {
-        load_sched(a.keys.table + 44, dk0);
+        load_sched(a.keys, 0, 1, dk0);
     } else {
         dk_id = ~0u;
     }
@@ -986,29 +854,19 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
         if (SESS && base >= sess_next) {  // (make_keysel checked every session is in the table)
             sess++;
             sess_next += a.sess_blocks;
-            load_sched(a.keys.table + (uint64_t)sess * kSchedWords + 44, dk0);
+            load_sched(a.keys, sess, 1, dk0);
         }
-#if !CYAES_DEC_PREFETCH  // A/B (tools/ab.py): prefetching the next step costs ~1% here
+        // (Issuing the next step's loads before this step's rounds measured ~1 %
+        // slower: the LDS binds, and the other 15 waves hide the loads.)
         carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv);
         if (base + 128 * R <= end) flat_load<true>(a, lane, base + 64 * R, end, c, pv);
-#else
-        // Issue the next step's loads before this step's rounds.
-        uint4 cn[R], pvn[R];
-        const bool more = base + 128 * R <= end;
-        if (more) flat_load<true>(a, lane, base + 64 * R, end, cn, pvn);
-        carry = flat_step<KEYED, BIG, true>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv);
-        if (more) {
-#pragma unroll
-            for (int k = 0; k < R; k++) { c[k] = cn[k]; pv[k] = pvn[k]; }
-        }
-#endif
         prio_feedback(leadp, ++prog, kDecPrioDiv);
         ps.bpos += a.step_r;
         ps.bp += a.step_q;
         if (ps.bpos >= a.bpp.d) { ps.bpos -= a.bpp.d; ps.bp++; }
     }
     if (base < end) {
-        if (SESS && base >= sess_next) load_sched(a.keys.table + (uint64_t)(sess + 1) * kSchedWords + 44, dk0);
+        if (SESS && base >= sess_next) load_sched(a.keys, sess + 1, 1, dk0);
         flat_load<false>(a, lane, base, end, c, pv);
         flat_step<KEYED, BIG, false>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv);
     }
@@ -1056,10 +914,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         (uint64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t G = a.group;
     const uint64_t ngroups = (a.npayloads + G - 1) / G;
+    const Ext iv_in_e = iv_ext(a.iv_in, a.npayloads), iv_out_e = iv_ext(a.iv_out, a.npayloads);
     uint32_t dk0[44];
     uint32_t dk_id = ~0u;  // session whose schedule dk0 holds
     if (!KEYED) {
-        load_sched(a.keys.table + 44, dk0);
+        load_sched(a.keys, 0, 1, dk0);
         dk_id = 0;
     }
     for (uint64_t grp = wave0; grp < ngroups; grp += nwaves) {
@@ -1067,12 +926,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         const uint32_t gn = (uint32_t)min<uint64_t>(G, a.npayloads - p0);
         const bool holder = lane < gn;
         const uint64_t ph = p0 + lane;
-        const uint32_t nbh = holder ? a.nbytes[ph] >> 4 : 0u;
-        const uint64_t offh = holder ? a.offsets[ph] : 0ull;
-        const uint32_t kidh = KEYED ? key_index(a.keys, ph, holder, a.status) : 0u;
+        const uint32_t nbh = holder ? LD4(a.nbytes + ph, ext(a.nbytes, 4 * a.npayloads)) >> 4 : 0u;
+        const uint64_t offh = holder ? LD8(a.offsets + ph, ext(a.offsets, 8 * a.npayloads)) : 0ull;
+        const uint32_t kidh = KEYED ? key_index(a.keys, ph, a.npayloads, holder, a.status) : 0u;
         if (holder && nbh == 0 && a.iv_out)  // empty chain: the IV comes back unchanged
-            *reinterpret_cast<uint4*>(a.iv_out + 16 * ph) =
-                a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * ph) : default_iv();
+            ST16(a.iv_out + 16 * ph, iv_out_e, a.iv_in ? LD16(a.iv_in + 16 * ph, iv_in_e) : default_iv());
         // Regular group: every payload has nb0 >= 64 blocks and the offsets are
         // equally strided (a relay stream of MTU-sized packets: payload p at
         // o + p * packet size).  Then each lane walks its own (payload, block)
@@ -1081,8 +939,8 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         const uint32_t nb0 = __builtin_amdgcn_readfirstlane(nbh);  // lane 0 holds a payload
         const uint64_t off0 = rlane64(offh, 0);
         const uint64_t ostr = gn > 1 ? rlane64(offh, 1) - off0 : 0;
-        const bool regular = CYAES_RAGGED_REGULAR && nb0 >= 64 &&
-                             __ballot(holder && (nbh != nb0 || offh != off0 + (uint64_t)lane * ostr)) == 0;
+        const bool regular =
+            nb0 >= 64 && __ballot(holder && (nbh != nb0 || offh != off0 + (uint64_t)lane * ostr)) == 0;
         uint32_t jt = 0, rt = lane - 64u;  // regular: this lane's payload and block; the first row adds 64
         // Inclusive prefix of the group's block counts (64-bit: payloads may be up to 2^28 blocks).
         uint64_t incl = nbh;
@@ -1098,7 +956,6 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         const uint64_t total = regular ? (uint64_t)gn * nb0 : rlane64(incl, 63);  // lanes >= gn add 0
         uint4 carry = make_uint4(0, 0, 0, 0);
         for (uint64_t base = 0; base < total; base += 64 * R) {
-            if (!CYAES_RAGGED_PRIO_LATE) prio_feedback(leadp, ++prog, kDecPrioDiv);
             uint4 c[R], pv[R];
             uint32_t jr[R], rr[R];
             uint64_t orow[R];
@@ -1148,17 +1005,29 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                 }
                 jr[k] = j;
             }
+            // Extent of each row's payload (bounds build only: a lane's payload
+            // j's bytes; an invalid lane loads row 0 lane 0's block, below).
+            Ext re[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                if constexpr (CYAES_BOUNDS_CHECK) {
+                    const uint32_t j = valid[k] ? jr[k] : __builtin_amdgcn_readfirstlane(jr[0]);
+                    re[k] = ext(a.in + bperm64(offh, j), 16ull * bperm(nbh, j));
+                } else {
+                    re[k] = Ext{nullptr, nullptr};
+                }
+            }
             // All four rows' loads back to back, unconditionally: a lane past the
             // group's end loads row 0 lane 0's block (always valid) and its result
             // is never used (a valid lane's predecessor is valid).  A load under
             // `valid ? load : 0` joined the branches with a vmcnt(0) wait per row.
             const uint64_t safe = rlane64(orow[0], 0);
 #pragma unroll
-            for (int k = 0; k < R; k++) c[k] = ldu(a.in + (valid[k] ? orow[k] : safe));
+            for (int k = 0; k < R; k++) c[k] = LD16U(a.in + (valid[k] ? orow[k] : safe), re[k]);
             // The progress atomic (a global word: the decrypt image fills the LDS) goes
             // out after the step's loads, so its round trip overlaps theirs instead of
             // delaying them (A/B: -1 % on relay streams, profiles/r02/ab_ragged_prio_late.txt).
-            if (CYAES_RAGGED_PRIO_LATE) prio_feedback(leadp, ++prog, kDecPrioDiv);
+            prio_feedback(leadp, ++prog, kDecPrioDiv);
             pv[0] = shr1(c[0], carry);
 #pragma unroll
             for (int k = 1; k < R; k++)
@@ -1166,11 +1035,10 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 const uint64_t p = p0 + jr[k];
-                if (valid[k] && rr[k] == 0)
-                    pv[k] = a.iv_in ? *reinterpret_cast<const uint4*>(a.iv_in + 16 * p) : default_iv();
+                if (valid[k] && rr[k] == 0) pv[k] = a.iv_in ? LD16(a.iv_in + 16 * p, iv_in_e) : default_iv();
                 if (a.iv_out) {  // (uniform branch: every lane runs the bpermute; one from an inactive lane reads 0)
                     const uint32_t nbj = regular ? nb0 : bperm(nbh, jr[k]);
-                    if (valid[k] && rr[k] + 1 == nbj) *reinterpret_cast<uint4*>(a.iv_out + 16 * p) = c[k];
+                    if (valid[k] && rr[k] + 1 == nbj) ST16(a.iv_out + 16 * p, iv_out_e, c[k]);
                 }
             }
             if (!KEYED) {
@@ -1185,7 +1053,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                 for (int k = 0; k < R; k++) same = same && (!valid[k] || kid[k] == k0);
                 if (__ballot(!same) == 0) {  // one session in the whole step (the common case)
                     if (k0 != dk_id) {
-                        load_sched(a.keys.table + (uint64_t)k0 * kSchedWords + 44, dk0);
+                        load_sched(a.keys, k0, 1, dk0);
                         dk_id = k0;
                     }
                     dec_cbc<R>(lds, lo, dk0, c, pv);
@@ -1200,7 +1068,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                             if (pending && kid[k] == ku) {
                                 pending = false;
                                 uint32_t dk[44];
-                                load_sched(a.keys.table + (uint64_t)ku * kSchedWords + 44, dk);
+                                load_sched(a.keys, ku, 1, dk);
                                 const uint4 cc[1] = {c[k]};
                                 uint4 dd[1] = {pv[k]};
                                 dec_cbc<1>(lds, lo, dk, cc, dd);
@@ -1211,8 +1079,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                 }
             }
 #pragma unroll
-            for (int k = 0; k < R; k++)
-                if (valid[k]) stu(a.out + orow[k], pv[k]);
+            for (int k = 0; k < R; k++) {
+                Ext we = re[k];
+                if constexpr (CYAES_BOUNDS_CHECK) we = ext(a.out + (we.lo - a.in), we.hi - we.lo);
+                if (valid[k]) ST16U(a.out + orow[k], we, pv[k]);
+            }
             carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
         }
     }
@@ -1226,7 +1097,8 @@ __global__ void k_boundary_snapshot(const uint4* in, uint64_t nblocks, uint64_t 
     if (w >= nwaves) return;
     const uint64_t begin = w * bpw;
     if (begin == 0 || begin >= nblocks) return;
-    if (begin % bpp.d != 0) boundary[w] = in[begin - 1];
+    if (begin % bpp.d != 0)
+        ST16(boundary + w, ext(boundary, 16 * nwaves), LD16(in + (begin - 1), ext(in, 16 * nblocks)));
 }
 
 // ---- key schedule (Rijndael::Rijndael, cyr_rijndael.cpp:507-572) ----------
@@ -1402,5 +1274,16 @@ extern "C" int cyaes_debug_probe(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cyaes::g_probe), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
     static const unsigned long long zero[8] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(cyaes::g_probe), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#if CYAES_BOUNDS_CHECK
+// Reads and clears the bounds record: out[4] = misses, first miss's source
+// line in this file, its offset from the extent's start, the extent's size.
+extern "C" int cyaes_debug_bounds(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cyaes::g_bounds), sizeof(unsigned long long) * 4) != hipSuccess) return -1;
+    static const unsigned long long zero[4] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(cyaes::g_bounds), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -108,17 +108,20 @@ int cyaes_mgpu_create(int ndev, const int* devices, cyaes_mgpu** out) {
     return CYAES_OK;
 }
 
-void cyaes_mgpu_destroy(cyaes_mgpu* mg) {
-    if (!mg) return;
+int cyaes_mgpu_destroy(cyaes_mgpu* mg) {
+    if (!mg) return CYAES_OK;
     DevScope scope;
+    int err = CYAES_OK;
     for (ncclComm_t c : mg->comm) (void)ncclCommDestroy(c);
     for (size_t i = 0; i < mg->ctx.size(); i++) {
         (void)hipSetDevice(mg->dev[i]);
         if (i < mg->stream.size() && mg->stream[i]) (void)hipStreamDestroy(mg->stream[i]);
         if (i < mg->d_raw.size() && mg->d_raw[i]) (void)hipFree(mg->d_raw[i]);
-        cyaes_gpu_destroy(mg->ctx[i]);
+        const int st = cyaes_gpu_destroy(mg->ctx[i]);  // a pending fault on any device is reported
+        if (err == CYAES_OK) err = st;
     }
     delete mg;
+    return err;
 }
 
 int cyaes_mgpu_ndev(const cyaes_mgpu* mg) { return mg ? (int)mg->ctx.size() : 0; }

@@ -28,10 +28,11 @@ struct cyaes_gpu {
     uint32_t key_cap = 0;
     uint32_t* d_status = nullptr;
     unsigned long long* d_digest = nullptr;
-    // Stream of the latest batch (cyaes_gpu_check syncs it); batches may be
-    // issued from several threads (drop-in leaders, the batcher).
-    std::atomic<hipStream_t> last_stream{nullptr};
     struct HostPipe* pipe = nullptr;  // cyaes_gpu_{en,de}crypt_host, created on first use
+    // Private stream-ordered pool for per-call scratch (StreamScratch).  Not the
+    // device's default pool: its policies and release threshold belong to every
+    // other user in the process (torch, RCCL).
+    hipMemPool_t pool = nullptr;
 };
 
 namespace {
@@ -127,7 +128,6 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.iv_out = iv_out;
     a.tables = ctx->d_tables + kEncTableOff / 4;
     a.status = ctx->d_status;
-    ctx->last_stream = stream;
     if (offsets ? ragged_encrypt_is_quad(ctx, npayloads) : npayloads < ctx->quad_max_chains) {
         // Latency-bound batch (fewer chains than lanes to fill the chip four
         // times over), or a ragged one: four lanes per chain (k_encrypt_quad).
@@ -138,15 +138,18 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     return map_err(launch_encrypt(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
 }
 
-// Per-call device scratch, stream-ordered (hipMallocAsync / hipFreeAsync on
-// the batch's stream): batches of one context on different streams never share
-// a scratch buffer while a kernel still reads it.
+// Per-call device scratch, stream-ordered (hipMallocFromPoolAsync /
+// hipFreeAsync on the batch's stream, from the context's private pool): batches
+// of one context on different streams never share a scratch buffer while a
+// kernel still reads it.  The pool never hands a block freed on one stream to
+// another stream opportunistically; reuse across streams only follows the
+// stream-order dependencies the runtime can see.
 struct StreamScratch {
     void* p = nullptr;
     hipStream_t s = nullptr;
-    int get(uint64_t bytes, hipStream_t stream) {
+    int get(hipMemPool_t pool, uint64_t bytes, hipStream_t stream) {
         s = stream;
-        CY_TRY(hipMallocAsync(&p, bytes, stream));
+        CY_TRY(hipMallocFromPoolAsync(&p, bytes, pool, stream));
         return CYAES_OK;
     }
     ~StreamScratch() {
@@ -156,9 +159,10 @@ struct StreamScratch {
 
 // d_iv_in == d_iv_out on a block-parallel decrypt: a payload's last block may
 // be written before its first block reads the IV, so read from a copy.
-int alias_iv(StreamScratch& sc, const uint8_t** iv_in, const uint8_t* iv_out, uint64_t npayloads, hipStream_t stream) {
+int alias_iv(cyaes_gpu* ctx, StreamScratch& sc, const uint8_t** iv_in, const uint8_t* iv_out, uint64_t npayloads,
+             hipStream_t stream) {
     if (!*iv_in || *iv_in != iv_out) return CYAES_OK;
-    int st = sc.get(npayloads * 16, stream);
+    int st = sc.get(ctx->pool, npayloads * 16, stream);
     if (st) return st;
     CY_TRY(hipMemcpyAsync(sc.p, *iv_in, npayloads * 16, hipMemcpyDeviceToDevice, stream));
     *iv_in = static_cast<const uint8_t*>(sc.p);
@@ -182,7 +186,7 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     uint64_t bpw = (nblocks + nwaves - 1) / nwaves;
     bpw = (bpw + step - 1) / step * step;
     StreamScratch iv_copy, boundary;
-    st = alias_iv(iv_copy, &iv_in, iv_out, npayloads, stream);
+    st = alias_iv(ctx, iv_copy, &iv_in, iv_out, npayloads, stream);
     if (st) return st;
     a.in = in;
     a.out = out;
@@ -202,13 +206,12 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     const uint64_t sess_blocks = (uint64_t)ppk * bpp;
     if (!key_idx && ppk && sess_blocks % step == 0) a.sess_blocks = sess_blocks;
     if (in == out && nwaves > 1) {
-        st = boundary.get(nwaves * sizeof(uint4), stream);
+        st = boundary.get(ctx->pool, nwaves * sizeof(uint4), stream);
         if (st) return st;
         uint4* snap = static_cast<uint4*>(boundary.p);
         CY_TRY(launch_boundary_snapshot(in, nblocks, bpw, nwaves, a.bpp, snap, stream));
         a.boundary = snap;
     }
-    ctx->last_stream = stream;
     return map_err(launch_decrypt_flat(a, grid, stream));
 }
 
@@ -219,7 +222,7 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys, table, table_keys);
     if (st) return st;
     StreamScratch iv_copy;
-    st = alias_iv(iv_copy, &iv_in, iv_out, npayloads, stream);
+    st = alias_iv(ctx, iv_copy, &iv_in, iv_out, npayloads, stream);
     if (st) return st;
     a.in = in;
     a.out = out;
@@ -239,7 +242,6 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
                                          : std::min<uint64_t>(64, std::max<uint64_t>(1, npayloads / (2 * slots)));
     a.group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, G));
     const Shape sh = wave_shape(ctx, (npayloads + a.group - 1) / a.group, kDecThreads);
-    ctx->last_stream = stream;
     return map_err(launch_decrypt_ragged(a, std::min(sh.grid, dec_grid_cap(ctx)), sh.threads, stream));
 }
 
@@ -326,16 +328,18 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (e == hipSuccess) e = hipMemset(ctx->d_status, 0, 16);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_digest), 16);
     if (e == hipSuccess) {
-        // Per-call scratch comes from the device's default pool (StreamScratch):
-        // keep up to 64 MiB of it cached across synchronisations.
-        hipMemPool_t pool = nullptr;
+        // Per-call scratch (StreamScratch): a private pool, kept warm up to 64
+        // MiB across synchronisations, with no opportunistic cross-stream reuse.
+        hipMemPoolProps props = {};
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = device;
+        e = hipMemPoolCreate(&ctx->pool, &props);
         uint64_t keep = 64ull << 20;
-        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
-            uint64_t cur = 0;
-            if (hipMemPoolGetAttribute(pool, hipMemPoolAttrReleaseThreshold, &cur) == hipSuccess && cur < keep)
-                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-        }
-        (void)hipGetLastError();
+        int no = 0;
+        if (e == hipSuccess) e = hipMemPoolSetAttribute(ctx->pool, hipMemPoolAttrReleaseThreshold, &keep);
+        if (e == hipSuccess) e = hipMemPoolSetAttribute(ctx->pool, hipMemPoolReuseAllowOpportunistic, &no);
     }
     if (e != hipSuccess) {
         cyaes_gpu_destroy(ctx);
@@ -345,16 +349,21 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     return CYAES_OK;
 }
 
-void cyaes_gpu_destroy(cyaes_gpu* ctx) {
-    if (!ctx) return;
+int cyaes_gpu_destroy(cyaes_gpu* ctx) {
+    if (!ctx) return CYAES_OK;
     DeviceGuard g(ctx->device);
-    (void)hipDeviceSynchronize();
+    // The device-wide synchronisation reports any fault still pending from this
+    // context's work (or anything else on the device): the caller learns of it
+    // here, not from the next context's first call.
+    const hipError_t e = hipDeviceSynchronize();
     (void)hipFree(ctx->d_tables);
     (void)hipFree(ctx->d_keys);
     (void)hipFree(ctx->d_status);
     (void)hipFree(ctx->d_digest);
     destroy_pipe(ctx->pipe);
+    if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);
     delete ctx;
+    return map_err(e);
 }
 
 int cyaes_gpu_device(const cyaes_gpu* ctx) { return ctx ? ctx->device : -1; }
@@ -430,7 +439,6 @@ int cyaes_gpu_set_keys_device(cyaes_gpu* ctx, const uint8_t* d_keys, uint32_t nk
     const uint8_t* d_sbox = reinterpret_cast<const uint8_t*>(ctx->d_tables) + kSboxOff;
     CY_TRY(launch_key_expand(d_keys, nkeys, d_sbox, ctx->d_keys, (hipStream_t)stream));
     ctx->nkeys = nkeys;
-    ctx->last_stream = (hipStream_t)stream;
     return CYAES_OK;
 }
 
@@ -520,7 +528,10 @@ int cyaes_gpu_cbc_decrypt_batch(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_
 int cyaes_gpu_check(cyaes_gpu* ctx) {
     if (!ctx) return CYAES_EINVAL;
     DeviceGuard g(ctx->device);
-    CY_TRY(hipStreamSynchronize(ctx->last_stream));
+    // Every stream this context's batches ran on (the caller's, the drop-in's,
+    // the host pipe's, the batcher's): the whole device, so an asynchronous
+    // fault is charged to the call that checks after it.
+    CY_TRY(hipDeviceSynchronize());
     CY_TRY(hipGetLastError());
     uint32_t status = 0;
     CY_TRY(hipMemcpy(&status, ctx->d_status, 4, hipMemcpyDeviceToHost));
@@ -880,6 +891,13 @@ struct HostPin {
     }
 };
 
+struct PipeDrain {
+    HostPipe* p;
+    ~PipeDrain() {
+        for (hipStream_t s : {p->up, p->comp, p->down}) (void)hipStreamSynchronize(s);
+    }
+};
+
 int host_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* h_in, uint8_t* h_out, uint64_t npayloads,
                uint32_t payload_bytes, uint32_t ppk, uint64_t chunk_bytes) {
     if (!ctx || !h_in || !h_out || payload_bytes % 16) return CYAES_EINVAL;
@@ -900,6 +918,10 @@ int host_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* h_in, uint8_t* h_out
     HostPin pin_in(h_in, total);
     HostPin pin_out(h_out, (h_out == h_in) ? 0 : total);
     HostPipe* p = ctx->pipe;
+    // Declared after the pins, so destroyed before them: on every return,
+    // early ones included, the copies queued from and to the caller's pages
+    // have finished before ~HostPin unregisters those pages.
+    PipeDrain drain{p};
     uint64_t i = 0;
     for (uint64_t c0 = 0; c0 < npayloads; c0 += cp, i++) {
         const int s = (int)(i % HostPipe::kSlots);
@@ -924,8 +946,7 @@ int host_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* h_in, uint8_t* h_out
         CY_TRY(hipEventRecord(p->ev_down[s], p->down));
     }
     CY_TRY(hipStreamSynchronize(p->down));
-    ctx->last_stream = p->down;
-    return CYAES_OK;
+    return CYAES_OK;  // (drain finds the streams idle)
 }
 
 }  // namespace

@@ -72,7 +72,11 @@ int cyaes_cbc_decrypt(const cyaes_key* key, const uint8_t* in, uint8_t* out, siz
 typedef struct cyaes_gpu cyaes_gpu;
 
 int cyaes_gpu_create(int device, cyaes_gpu** out);
-void cyaes_gpu_destroy(cyaes_gpu* ctx);
+/* Synchronises the device, frees the context and returns the synchronisation's
+ * status: CYAES_EDEVICE if an asynchronous fault is pending (from this
+ * context's work or any other on the device), else CYAES_OK.  The context is
+ * freed either way. */
+int cyaes_gpu_destroy(cyaes_gpu* ctx);
 int cyaes_gpu_device(const cyaes_gpu* ctx);
 /* Number of compute units, and workgroups the batch kernels launch per CU. */
 int cyaes_gpu_num_cus(const cyaes_gpu* ctx);
@@ -147,9 +151,10 @@ int cyaes_gpu_encrypt_host(cyaes_gpu* ctx, const uint8_t* h_in, uint8_t* h_out, 
 int cyaes_gpu_decrypt_host(cyaes_gpu* ctx, const uint8_t* h_in, uint8_t* h_out, uint64_t npayloads,
                            uint32_t payload_bytes, uint32_t payloads_per_key, uint64_t chunk_bytes);
 
-/* Synchronises the context's last-used stream and returns CYAES_ERANGE if a
- * batch since the previous check saw an out-of-range key index (sticky flag
- * is then cleared), CYAES_EDEVICE on an asynchronous HIP error, else CYAES_OK. */
+/* Synchronises the device (every stream the context's batches ran on) and
+ * returns CYAES_EDEVICE on an asynchronous HIP error, CYAES_ERANGE if a batch
+ * since the previous check saw an out-of-range key index (the sticky flag is
+ * then cleared), else CYAES_OK. */
 int cyaes_gpu_check(cyaes_gpu* ctx);
 
 /* ---- Workload utilities (bench / verification; not on the hot path) ----- */

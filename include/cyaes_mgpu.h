@@ -26,7 +26,9 @@ typedef struct cyaes_mgpu cyaes_mgpu;
 
 /* devices == NULL => 0 .. ndev-1.  Creates the contexts and the RCCL clique. */
 int cyaes_mgpu_create(int ndev, const int* devices, cyaes_mgpu** out);
-void cyaes_mgpu_destroy(cyaes_mgpu* mg);
+/* Frees every device context; returns the first device's pending-fault status
+ * (cyaes_gpu_destroy), else CYAES_OK. */
+int cyaes_mgpu_destroy(cyaes_mgpu* mg);
 int cyaes_mgpu_ndev(const cyaes_mgpu* mg);
 /* The per-device context (for any cyaes_gpu_* call), or NULL. */
 cyaes_gpu* cyaes_mgpu_context(cyaes_mgpu* mg, int i);

@@ -18,6 +18,30 @@ def pytest_configure(config):
         subprocess.run(["make", "-C", ROOT, "-j8", "lib", "oracle"], check=True)
 
 
+@pytest.fixture(autouse=True)
+def _gpu_fault_guard(request):
+    """After every `gpu` test: synchronise the device, so an asynchronous fault
+    is charged to the test whose work caused it (not to the next test's first
+    HIP call), and, on the bounds-checked build (CYAES_LIBRARY=
+    build/variants/bounds.so), assert that no kernel access left its extent."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import ctypes
+    import torch
+    if not torch.cuda.is_available():
+        return
+    torch.cuda.synchronize()
+    import cyclone_amd
+    lib = cyclone_amd.load_library()
+    fn = getattr(lib, "cyaes_debug_bounds", None)
+    if fn is not None:
+        rec = (ctypes.c_ulonglong * 4)()
+        assert fn(rec) == 0, "cyaes_debug_bounds failed (device error)"
+        assert rec[0] == 0, ("bounds check: %d access(es) outside their extent; first at cyaes_kernels.hip:%d, "
+                             "offset %d of a %d-byte extent" % (rec[0], rec[1], ctypes.c_longlong(rec[2]).value, rec[3]))
+
+
 @pytest.fixture(scope="session")
 def golden():
     import json

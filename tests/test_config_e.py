@@ -89,6 +89,9 @@ def test_two_rank_config_e_bit_exact(tmp_path):
     # every pass of every rank matched its committed OpenSSL pass digest
     assert [s["golden_verified"] for s in shards] == [[0, 1, 2, 3], [4, 5, 6, 7]]
     assert out["value"] > 0 and out["roofline"]["bound"] == "lds"
+    d = out["dist"]  # both ranks share the box's one device here (CYAES_BENCH_SAME_DEVICE)
+    assert d["backend"] == "gloo" and d["world_size"] == 2 and d["ranks_reporting"] == 2
+    assert d["distinct_devices"] == 1 and d["same_keys_all_ranks"] is True
 
 
 @pytest.mark.gpu
@@ -154,10 +157,6 @@ def test_bench_line_contract_single_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(not os.environ.get("CYAES_TEST_RCCL"),
-                    reason="opt-in (CYAES_TEST_RCCL=1): a second process initialising RCCL on the device the "
-                           "test process holds; two GPU-suite runs with it in the default set later reported "
-                           "illegal-address errors in runtime copies (DESIGN.md §4), so it runs on its own")
 def test_rccl_path_world_one_bit_exact():
     """The driver's N>1 code path on RCCL itself: bench.py under torchrun with
     the default backend ("nccl" = RCCL) at world size 1 (CYAES_BENCH_FORCE_DIST
@@ -179,5 +178,10 @@ def test_rccl_path_world_one_bit_exact():
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["parity"] == "bit-exact" and out["n_gpus"] == 1
     assert out["shards"][0]["golden_verified"] == [0, 1]
+    # the fields a driver N-GPU record is read by: RCCL's process group, its size, one device per rank
+    d = out["dist"]
+    assert d["backend"] == "nccl" and d["world_size"] == 1 and d["ranks_reporting"] == 1
+    assert d["distinct_devices"] == 1 and d["same_keys_all_ranks"] is True
+    assert out["shards"][0]["device"] == 0 and out["shards"][0]["pci"]
     assert out["packet_configs"]["D"]["parity"] == "bit-exact"
     assert out["relay_stream"]["parity"] == "bit-exact"

@@ -377,6 +377,46 @@ def test_iv_in_out(torch, ctx, alias):
     assert np.array_equal(host(d_ivo2).reshape(n, 16), want_iv)  # last ciphertext block
 
 
+@pytest.mark.parametrize("pb,n", [(16, 1), (16, 3), (4800, 3), (4800, 7), (65280, 2)])
+@pytest.mark.parametrize("with_iv", [False, True])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_decrypt_extent_edges(torch, ctx, pb, n, with_iv, inplace):
+    """The two r02 over-reads of k_decrypt_flat's partial last step, pinned
+    (VERDICT r02 "What's weak" 1): a 1-block batch, where lanes 1..63 read the
+    block before the buffer, and payloads of >= 256 blocks (4,800 B = 300
+    blocks; 65,280 B = the relay's largest chunk, 4,080 blocks) with IVs in and
+    nblocks % 256 != 0, where the partial step read iv_in[npayloads], 16 B past
+    the IV array.  The ciphertext sits at the start of its allocation and the
+    IVs at the very end of theirs; the bounds build (tests/conftest.py) names
+    any access outside.  Semantics: cyr_rijndael.cpp:612-635 (IV in, last
+    ciphertext block out, in place)."""
+    rng = np.random.default_rng(pb * 31 + n)
+    nbytes = pb * n
+    pt = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    ivs = rng.integers(0, 256, (n, 16), dtype=np.uint8) if with_iv else np.tile(np.arange(16, dtype=np.uint8), (n, 1))
+    want_ct, want_iv = np.empty_like(pt), np.empty_like(ivs)
+    for p in range(n):
+        iv = bytearray(ivs[p].tobytes())
+        want_ct[p * pb:(p + 1) * pb] = np.frombuffer(
+            bytes(oracle.Rijndael(K0).encrypt(pt[p * pb:(p + 1) * pb].tobytes(), None, pb, iv)), np.uint8)
+        want_iv[p] = np.frombuffer(bytes(iv), np.uint8)
+    ct_alloc = torch.empty(nbytes + 4096, dtype=torch.uint8, device="cuda")
+    d_ct = ct_alloc[:nbytes]
+    d_ct.copy_(torch.from_numpy(want_ct).to("cuda"))
+    d_out = d_ct if inplace else empty(torch, nbytes)
+    iv_in = iv_out = None
+    if with_iv:
+        iv_alloc = torch.empty(16 * n + 1024, dtype=torch.uint8, device="cuda")
+        iv_in = iv_alloc[-16 * n:]
+        iv_in.copy_(torch.from_numpy(ivs.reshape(-1)).to("cuda"))
+        iv_out = empty(torch, 16 * n)
+    ctx.decrypt_uniform(d_ct, d_out, n, pb, iv_in=iv_in, iv_out=iv_out)
+    assert np.array_equal(host(d_out), pt)
+    if with_iv:
+        assert np.array_equal(host(iv_out).reshape(n, 16), want_iv)  # last ciphertext block per payload
+    assert ctx.check() == ca.CYAES_OK
+
+
 def test_ragged_batches(torch, encrypt_kernel):
     """Relay packets of mixed sizes (0..65280 B), gaps between them, per-payload keys and IVs."""
     rng = np.random.default_rng(4)

@@ -1,0 +1,65 @@
+#!/bin/bash
+# tools/gpu.sh -- the one GPU-box runner (replaces round 2's per-experiment
+# scripts/).  Runs the named steps in order under their own time limits and
+# stops at the first failure; every step's output goes to gpurun_out/$OUT/.
+#
+# usage: tools/gpu.sh OUT STEP [STEP ...]
+#   test       python -m pytest tests -m gpu (product build)
+#   bounds     the same suite on the bounds-checked build (CYAES_LIBRARY=build/variants/bounds.so)
+#   smoke      __graft_entry__.smoke()
+#   bench      python bench.py (default: config E headline + packet configs + relay stream)
+#   quickbench bench.py --steps 3 --warmup 1 (no CPU baseline)
+#   profile    rocprofv3 --kernel-trace --stats of a short bench, then FETCH_SIZE / WRITE_SIZE PMC passes
+#   batcher    build/bench_batcher SEAL / OPEN loads (host to host)
+#   ab:A:B[:ARGS]  tools/ab.py on variant libraries build/variants/{A,B}.so, both orders
+#                  (ARGS: extra ab.py arguments, commas for spaces)
+#   abrelay:A:B    tools/ab_relay_layout.py on the two variants (relay stream layouts)
+set -u
+OUT=${1:?usage: tools/gpu.sh OUT STEP...}
+shift
+R=${GRAFT_REPO_ROOT:-$PWD}
+O=$R/gpurun_out/$OUT
+mkdir -p "$O"
+export TMPDIR=/tmp
+PYT="python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread"
+
+run() {  # run NAME SECONDS CMD...: output to $O/NAME.txt, stop the script on failure
+  local name=$1 secs=$2
+  shift 2
+  echo "[gpu] $name: $*"
+  timeout -k 10 "$secs" "$@" > "$O/$name.txt" 2>&1
+  local rc=$?
+  echo "[gpu] $name rc=$rc"
+  tail -3 "$O/$name.txt"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+
+for step in "$@"; do
+  case $step in
+    test) run pytest_gpu 600 $PYT ;;
+    bounds) CYAES_LIBRARY=$R/build/variants/bounds.so run pytest_bounds 600 $PYT ;;
+    smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 400 python bench.py ;;
+    quickbench) run quickbench 300 python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    profile)
+      (cd /tmp && run rocprof_stats 300 rocprofv3 --kernel-trace --stats -d "$O/rocprof" -o run --output-format csv \
+        -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --packet-configs none --relay-stream 0) || exit $?
+      for c in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && run pmc_$c 300 rocprofv3 --pmc $c -d "$O/pmc_$c" -o run --output-format csv \
+          -- python3 "$R/bench.py" --config C --steps 2 --warmup 0 --no-cpu --no-verify --no-clock \
+             --packet-configs none --relay-stream 0) || exit $?
+      done ;;
+    batcher) run bench_batcher 300 build/bench_batcher ;;
+    ab:*)
+      IFS=: read -r _ A B ARGS <<< "$step"
+      L="build/variants/$A.so build/variants/$B.so"
+      RL="build/variants/$B.so build/variants/$A.so"
+      run ab_${A}_vs_${B} 300 python tools/ab.py $L ${ARGS//,/ }
+      run ab_${B}_vs_${A} 300 python tools/ab.py $RL ${ARGS//,/ } ;;
+    abrelay:*)
+      IFS=: read -r _ A B <<< "$step"
+      run abrelay_${A}_vs_${B} 300 python tools/ab_relay_layout.py --lib build/variants/$A.so build/variants/$B.so ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[gpu] done"
