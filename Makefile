@@ -35,7 +35,7 @@ AOBJ     := $(BUILD)/cyaes_adler.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
 .PHONY: all lib mgpu oracle cpptest probe bounds microbench variant clean
-all: lib mgpu oracle cpptest probe bounds $(BUILD)/bench_batcher $(BUILD)/dropin_threads $(BUILD)/bitslice
+all: lib mgpu oracle cpptest probe bounds $(BUILD)/bench_batcher $(BUILD)/dropin_threads $(BUILD)/bitslice $(BUILD)/hostlink
 lib: $(LIB)
 mgpu: $(MGPU)
 oracle: $(ORACLE)
@@ -79,6 +79,10 @@ $(BUILD)/bench_batcher: tools/bench_batcher.cpp $(LIB) $(HDRS) | $(BUILD)
 
 $(BUILD)/dropin_threads: tools/dropin_threads.cpp $(LIB) $(HDRS) | $(BUILD)
 	$(CXX) -O2 -std=c++17 -Wall -pthread $(INC) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
+
+# Kernel-driven host<->HBM packet moves vs DMA (the batcher's zero-copy gather/scatter)
+$(BUILD)/hostlink: tools/hostlink.hip | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
 $(BUILD)/microbench: tools/microbench.hip | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -o $@ $<

@@ -81,12 +81,15 @@ __device__ __forceinline__ Ext ext(const void* p, uint64_t bytes) {
 }
 
 #if CYAES_BOUNDS_CHECK
+constexpr uint32_t kBoundsLines = 2048;    // misses per source line of this file
 __device__ unsigned long long g_bounds[4];  // misses, first miss's line, its offset from lo, the extent's size
+__device__ unsigned int g_bounds_lines[kBoundsLines];
 __device__ uint4 g_bounds_sink[64];
 template <typename T>
 __device__ __forceinline__ T* bchk(T* p, Ext e, uint32_t bytes, uint32_t line) {
     const uint8_t* b = reinterpret_cast<const uint8_t*>(p);
     if (e.lo && b >= e.lo && b + bytes <= e.hi) return p;
+    atomicAdd(&g_bounds_lines[line % kBoundsLines], 1u);
     if (atomicAdd(&g_bounds[0], 1ull) == 0) {
         g_bounds[1] = line;
         g_bounds[2] = (unsigned long long)(b - e.lo);
@@ -1008,10 +1011,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
             // Extent of each row's payload (bounds build only: a lane's payload
             // j's bytes; an invalid lane loads row 0 lane 0's block, below).
             Ext re[R];
+            const uint32_t j00 = __builtin_amdgcn_readlane(jr[0], 0);  // (not readfirstlane: exec may be partial)
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 if constexpr (CYAES_BOUNDS_CHECK) {
-                    const uint32_t j = valid[k] ? jr[k] : __builtin_amdgcn_readfirstlane(jr[0]);
+                    const uint32_t j = valid[k] ? jr[k] : j00;
                     re[k] = ext(a.in + bperm64(offh, j), 16ull * bperm(nbh, j));
                 } else {
                     re[k] = Ext{nullptr, nullptr};
@@ -1279,11 +1283,19 @@ extern "C" int cyaes_debug_probe(unsigned long long* out) {
 
 #if CYAES_BOUNDS_CHECK
 // Reads and clears the bounds record: out[4] = misses, first miss's source
-// line in this file, its offset from the extent's start, the extent's size.
+// line in this file, its offset from the extent's start, the extent's size;
+// then up to 8 (line, misses) pairs of the lines that missed in out[4..20).
 extern "C" int cyaes_debug_bounds(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cyaes::g_bounds), sizeof(unsigned long long) * 4) != hipSuccess) return -1;
+    static unsigned int lines[cyaes::kBoundsLines];
+    if (hipMemcpyFromSymbol(lines, HIP_SYMBOL(cyaes::g_bounds_lines), sizeof(lines)) != hipSuccess) return -1;
+    for (int i = 4; i < 20; i++) out[i] = 0;
+    for (uint32_t l = 0, k = 4; l < cyaes::kBoundsLines && k < 20; l++)
+        if (lines[l]) out[k++] = l, out[k++] = lines[l];
     static const unsigned long long zero[4] = {};
+    static const unsigned int zl[cyaes::kBoundsLines] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cyaes::g_bounds_lines), zl, sizeof(zl)) != hipSuccess) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(cyaes::g_bounds), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif

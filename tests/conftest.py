@@ -36,10 +36,12 @@ def _gpu_fault_guard(request):
     lib = cyclone_amd.load_library()
     fn = getattr(lib, "cyaes_debug_bounds", None)
     if fn is not None:
-        rec = (ctypes.c_ulonglong * 4)()
+        rec = (ctypes.c_ulonglong * 20)()
         assert fn(rec) == 0, "cyaes_debug_bounds failed (device error)"
+        lines = {int(rec[i]): int(rec[i + 1]) for i in range(4, 20, 2) if rec[i + 1]}
         assert rec[0] == 0, ("bounds check: %d access(es) outside their extent; first at cyaes_kernels.hip:%d, "
-                             "offset %d of a %d-byte extent" % (rec[0], rec[1], ctypes.c_longlong(rec[2]).value, rec[3]))
+                             "offset %d of a %d-byte extent; misses by line: %s"
+                             % (rec[0], rec[1], ctypes.c_longlong(rec[2]).value, rec[3], lines))
 
 
 @pytest.fixture(scope="session")

@@ -11,6 +11,7 @@
 #   quickbench bench.py --steps 3 --warmup 1 (no CPU baseline)
 #   profile    rocprofv3 --kernel-trace --stats of a short bench, then FETCH_SIZE / WRITE_SIZE PMC passes
 #   batcher    build/bench_batcher SEAL / OPEN loads (host to host)
+#   hostlink   build/hostlink: kernel-driven packet gather/scatter over PCIe vs DMA
 #   ab:A:B[:ARGS]  tools/ab.py on variant libraries build/variants/{A,B}.so, both orders
 #                  (ARGS: extra ab.py arguments, commas for spaces)
 #   abrelay:A:B    tools/ab_relay_layout.py on the two variants (relay stream layouts)
@@ -50,6 +51,7 @@ for step in "$@"; do
              --packet-configs none --relay-stream 0) || exit $?
       done ;;
     batcher) run bench_batcher 300 build/bench_batcher ;;
+    hostlink) run hostlink 240 build/hostlink ;;
     ab:*)
       IFS=: read -r _ A B ARGS <<< "$step"
       L="build/variants/$A.so build/variants/$B.so"
