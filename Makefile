@@ -25,6 +25,7 @@ BOUNDS   := $(BUILD)/variants/bounds.so
 
 KSRC     := cyclone_amd/csrc/cyaes_kernels.hip
 ASRC     := cyclone_amd/csrc/cyaes_adler.hip
+BSRC     := cyclone_amd/csrc/cyaes_batch_kernels.hip
 HSRC     := cyclone_amd/csrc/cyaes_runtime.cpp cyclone_amd/csrc/cyaes_tables.cpp cyclone_amd/csrc/cyr_rijndael.cpp \
             cyclone_amd/csrc/cyaes_relay.cpp cyclone_amd/csrc/cyaes_batcher.cpp
 HDRS     := include/cyaes.h include/cyaes_relay.h include/cyaes_batch.h include/cyclone_amd/cyr_rijndael.h cyclone_amd/csrc/cyaes_internal.h \
@@ -32,6 +33,7 @@ HDRS     := include/cyaes.h include/cyaes_relay.h include/cyaes_batch.h include/
 
 KOBJ     := $(BUILD)/cyaes_kernels.o
 AOBJ     := $(BUILD)/cyaes_adler.o
+BOBJ     := $(BUILD)/cyaes_batch_kernels.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
 .PHONY: all lib mgpu oracle cpptest probe bounds microbench variant clean
@@ -52,10 +54,13 @@ $(KOBJ): $(KSRC) $(HDRS) | $(BUILD)
 $(AOBJ): $(ASRC) include/cyaes_adler32.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BOBJ): $(BSRC) $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/%.o: cyclone_amd/csrc/%.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
 
-$(LIB): $(KOBJ) $(AOBJ) $(HOBJ)
+$(LIB): $(KOBJ) $(AOBJ) $(BOBJ) $(HOBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
 
 # Single-process multi-GPU front end: separate library so libcyaes.so does not pull in RCCL.
@@ -87,25 +92,25 @@ $(BUILD)/hostlink: tools/hostlink.hip | $(BUILD)
 $(BUILD)/microbench: tools/microbench.hip | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
-$(PROBE): $(KSRC) $(HDRS) $(HOBJ) $(AOBJ)
+$(PROBE): $(KSRC) $(HDRS) $(HOBJ) $(AOBJ) $(BOBJ)
 	mkdir -p $(BUILD)/variants
 	$(HIPCC) $(HIPFLAGS) -DCYAES_CLOCK_PROBE=1 -c $(KSRC) -o $(BUILD)/variants/clockprobe.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(BUILD)/variants/clockprobe.o $(AOBJ) $(HOBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(BUILD)/variants/clockprobe.o $(AOBJ) $(BOBJ) $(HOBJ)
 
-$(BOUNDS): $(KSRC) $(HDRS) $(HOBJ) $(AOBJ)
+$(BOUNDS): $(KSRC) $(HDRS) $(HOBJ) $(AOBJ) $(BOBJ)
 	mkdir -p $(BUILD)/variants
 	$(HIPCC) $(HIPFLAGS) -DCYAES_BOUNDS_CHECK=1 -c $(KSRC) -o $(BUILD)/variants/bounds.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(BUILD)/variants/bounds.o $(AOBJ) $(HOBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(BUILD)/variants/bounds.o $(AOBJ) $(BOBJ) $(HOBJ)
 
 # Bitsliced decrypt prototype (measurement tool)
 $(BUILD)/bitslice: tools/bitslice.hip tools/bitslice_gen.h $(LIB) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
 
 # A/B variants: make variant NAME=x DEFS="-DFOO=1" -> build/variants/x.so
-variant: $(HOBJ) $(AOBJ) | $(BUILD)
+variant: $(HOBJ) $(AOBJ) $(BOBJ) | $(BUILD)
 	mkdir -p $(BUILD)/variants
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(KSRC) -o $(BUILD)/variants/$(NAME).o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/$(NAME).so $(BUILD)/variants/$(NAME).o $(AOBJ) $(HOBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/$(NAME).so $(BUILD)/variants/$(NAME).o $(AOBJ) $(BOBJ) $(HOBJ)
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(MGPU) $(ORACLE)

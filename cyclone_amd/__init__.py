@@ -111,6 +111,9 @@ _SIGS = {
     "cyaes_batcher_submit_open": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp]),
     "cyaes_batcher_submit_many": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
     "cyaes_batcher_flush": (ctypes.c_int, [_vp]),
+    "cyaes_batcher_register_pool": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _u32p]),
+    "cyaes_batcher_unregister_pool": (ctypes.c_int, [_vp, ctypes.c_uint32]),
+    "cyaes_batcher_submit_pooled": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
     "cyaes_batcher_stats": (ctypes.c_int, [_vp, _u64p]),
 }
 
@@ -421,9 +424,18 @@ class BatchReq(ctypes.Structure):
                 ("out", _vp), ("size", ctypes.c_uint32), ("done", _DONE_FN), ("user", _vp)]
 
 
+class PoolReq(ctypes.Structure):
+    """struct cyaes_pool_req (cyaes_batcher_submit_pooled)."""
+
+    _fields_ = [("op", ctypes.c_int), ("slot", ctypes.c_uint32), ("conn_id", ctypes.c_int32), ("pool", ctypes.c_uint32),
+                ("in_off", ctypes.c_uint64), ("out_off", ctypes.c_uint64), ("size", ctypes.c_uint32),
+                ("done", _DONE_FN), ("user", _vp)]
+
+
 class BatcherConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("max_batch_bytes", ctypes.c_uint32),
-                ("max_delay_us", ctypes.c_uint32), ("inflight", ctypes.c_uint32), ("workers", ctypes.c_uint32)]
+                ("max_delay_us", ctypes.c_uint32), ("inflight", ctypes.c_uint32), ("workers", ctypes.c_uint32),
+                ("max_sessions", ctypes.c_uint32)]
 
 
 class Batcher:
@@ -433,9 +445,9 @@ class Batcher:
     alive by the batcher until the request completes.  `done(status)` runs on
     the batcher's completion thread."""
 
-    def __init__(self, device=0, max_batch_bytes=0, max_delay_us=0, inflight=0, workers=0, lib=None):
+    def __init__(self, device=0, max_batch_bytes=0, max_delay_us=0, inflight=0, workers=0, max_sessions=0, lib=None):
         self._lib = lib if lib is not None else load_library()
-        cfg = BatcherConfig(device, max_batch_bytes, max_delay_us, inflight, workers)
+        cfg = BatcherConfig(device, max_batch_bytes, max_delay_us, inflight, workers, max_sessions)
         h = _vp()
         _check(self._lib.cyaes_batcher_create(ctypes.byref(cfg), ctypes.byref(h)), "cyaes_batcher_create")
         self._h = h
@@ -544,6 +556,38 @@ class Batcher:
             arr[i] = BatchReq(op, slot, conn or 0, src.ptr, dst.ptr, size, self._cb, token)
         st = (ctypes.c_int * max(1, n))()
         self._lib.cyaes_batcher_submit_many(self._h, arr, n, st)
+        for i, token in enumerate(tokens):
+            if st[i]:
+                self._untrack(token)
+        return [int(st[i]) for i in range(n)]
+
+    def register_pool(self, buf):
+        """Registers a writable host buffer (bytearray, numpy array, ...) as a
+        zero-copy packet pool; returns its id.  The buffer is kept alive until
+        unregister_pool."""
+        b = _Buf(buf, True)
+        pool = ctypes.c_uint32()
+        _check(self._lib.cyaes_batcher_register_pool(self._h, b.ptr, b.n, ctypes.byref(pool)), "register_pool")
+        self._pools = getattr(self, "_pools", {})
+        self._pools[pool.value] = b
+        return pool.value
+
+    def unregister_pool(self, pool):
+        _check(self._lib.cyaes_batcher_unregister_pool(self._h, pool), "unregister_pool")
+        getattr(self, "_pools", {}).pop(pool, None)
+
+    def submit_pooled(self, reqs):
+        """reqs: [(op, slot, pool, in_off, out_off, size, done, conn_id)] by pool
+        offsets (cyaes_batcher_submit_pooled); returns the per-request status list."""
+        n = len(reqs)
+        arr = (PoolReq * max(1, n))()
+        tokens = []
+        for i, (op, slot, pool, in_off, out_off, size, done, conn) in enumerate(reqs):
+            token = self._track((), done)
+            tokens.append(token)
+            arr[i] = PoolReq(op, slot, conn or 0, pool, in_off, out_off or 0, size, self._cb, token)
+        st = (ctypes.c_int * max(1, n))()
+        self._lib.cyaes_batcher_submit_pooled(self._h, arr, n, st)
         for i, token in enumerate(tokens):
             if st[i]:
                 self._untrack(token)

@@ -1,0 +1,134 @@
+// cyaes_batch_kernels.hip -- the batching adapter's device-side gather and
+// scatter (include/cyaes_batch.h, cyaes_batcher.cpp).
+//
+// A batch is a list of request descriptors (BatchDesc, cyaes_internal.h).
+// Each names its input and output by DEVICE address: host memory the caller
+// registered as a packet pool (hipHostRegister, mapped), or the batcher's own
+// pinned bounce buffer for requests outside every pool.  The GPU moves the
+// bytes itself over PCIe -- one wave per request, 256 B (dwords) or 1 KiB
+// (dwordx4) contiguous per wave instruction -- so the host copies nothing:
+//   k_batch_gather : input -> the batch's HBM stage, building RELAY_FORWARD
+//                    packets for SEAL on the way (relay_local.cpp:189-201:
+//                    BE u16 size and id, RelayForwardMsg{id, size} in host
+//                    order, the chunk, 0xCE padding to 16, cye_packet.cpp:102),
+//                    and writes the ragged kernels' (offset, bytes, key) lists;
+//   (k_encrypt_quad / k_encrypt / k_decrypt_ragged run on the stage in HBM;)
+//   k_batch_scatter: stage -> outputs: the sealed packet (SEAL), the payload
+//                    decrypted in place behind the untouched header (OPEN,
+//                    relay_server.cpp:329), or the CBC output (ENCRYPT/DECRYPT).
+#include "cyaes_internal.h"
+#include "cyaes_relay.h"
+
+namespace cyaes {
+namespace {
+
+constexpr uint32_t kHead = CYAES_RELAY_HEADSIZE;          // Packet head: BE u16 size, BE u16 id (cye_packet.h:6-25)
+constexpr uint32_t kPayload = CYAES_RELAY_PAYLOAD_OFFSET;  // head + RelayForwardMsg{int32 id, int32 size}
+constexpr uint32_t kForwardId = CYAES_RELAY_FORWARD;       // relay_protocol.h:9-14
+constexpr uint8_t kPad = CYAES_RELAY_PAD;                  // Packet::_resize fill (cye_packet.cpp:102)
+
+// dst[0, n) = src[0, n), one wave: 16 B per lane when both ends and n are
+// 16-B aligned, else dwords when 4-B aligned (the tail bytes singly), else bytes.
+__device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t lane) {
+    const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
+    if (((a | n) & 15u) == 0) {
+        for (uint32_t o = 16 * lane; o < n; o += 1024)
+            *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(src + o);
+        return;
+    }
+    uint32_t body = 0;
+    if ((a & 3u) == 0) {
+        body = n & ~3u;
+        for (uint32_t o = 4 * lane; o < body; o += 256)
+            *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(src + o);
+    }
+    for (uint32_t o = body + lane; o < n; o += 64) dst[o] = src[o];
+}
+
+__device__ __forceinline__ bool is_relay(uint32_t op) { return op >= kOpRelaySeal; }
+
+// One wave per request (grid-stride).  Requests [0, ne) are the encrypt list
+// (ENCRYPT, SEAL), [ne, n) the decrypt list (DECRYPT, OPEN); list entry i of
+// the ragged kernels is request i (the decrypt kernel gets the lists from ne).
+__global__ void k_batch_gather(const BatchDesc* __restrict__ desc, uint32_t n, uint8_t* __restrict__ stage,
+                               uint64_t* __restrict__ offs, uint32_t* __restrict__ nbytes, uint32_t* __restrict__ kidx) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * (blockDim.x / 64);
+    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nw) {
+        const BatchDesc d = desc[i];
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(d.src);
+        uint8_t* s = stage + d.stage;
+        if (lane == 0) {
+            offs[i] = is_relay(d.op) ? d.stage + 16 : d.stage;  // relay payload 16-B aligned at stage + 16
+            nbytes[i] = d.crypt;
+            kidx[i] = d.key;
+        }
+        switch (d.op) {
+            case kOpEncrypt:
+            case kOpDecrypt:
+                wave_copy(s, src, d.size, lane);
+                break;
+            case kOpRelaySeal: {  // packet at stage + 4, so its payload (offset 12) is at stage + 16
+                uint8_t* pk = s + kHead;
+                if (lane == 0) {
+                    const uint32_t psize = 8 + d.crypt;
+                    pk[0] = (uint8_t)(psize >> 8);
+                    pk[1] = (uint8_t)psize;
+                    pk[2] = (uint8_t)(kForwardId >> 8);
+                    pk[3] = (uint8_t)kForwardId;
+                    *reinterpret_cast<int32_t*>(pk + 4) = d.conn;          // RelayForwardMsg::id
+                    *reinterpret_cast<int32_t*>(pk + 8) = (int32_t)d.size; // RelayForwardMsg::size
+                }
+                wave_copy(pk + kPayload, src, d.size, lane);
+                for (uint32_t o = d.size + lane; o < d.crypt; o += 64) pk[kPayload + o] = kPad;
+                break;
+            }
+            case kOpRelayOpen:  // the payload only: the header stays where it is
+                wave_copy(s + 16, src + kPayload, d.crypt, lane);
+                break;
+        }
+    }
+}
+
+__global__ void k_batch_scatter(const BatchDesc* __restrict__ desc, uint32_t n, const uint8_t* __restrict__ stage) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * (blockDim.x / 64);
+    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nw) {
+        const BatchDesc d = desc[i];
+        uint8_t* dst = reinterpret_cast<uint8_t*>(d.dst);
+        const uint8_t* s = stage + d.stage;
+        switch (d.op) {
+            case kOpEncrypt:
+            case kOpDecrypt:
+                wave_copy(dst, s, d.size, lane);
+                break;
+            case kOpRelaySeal:  // the whole packet: header, RelayForwardMsg, ciphertext
+                wave_copy(dst, s + kHead, kPayload + d.crypt, lane);
+                break;
+            case kOpRelayOpen:  // plaintext back behind the header (in place)
+                wave_copy(dst + kPayload, s + 16, d.crypt, lane);
+                break;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_batch_gather(const BatchDesc* d_desc, uint32_t n, uint8_t* d_stage, uint64_t* d_offs,
+                               uint32_t* d_nbytes, uint32_t* d_kidx, int max_waves, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t waves = n < (uint32_t)max_waves ? n : (uint32_t)max_waves;
+    hipLaunchKernelGGL(k_batch_gather, dim3((waves + 3) / 4), dim3(256), 0, stream, d_desc, n, d_stage, d_offs,
+                       d_nbytes, d_kidx);
+    return hipGetLastError();
+}
+
+hipError_t launch_batch_scatter(const BatchDesc* d_desc, uint32_t n, const uint8_t* d_stage, int max_waves,
+                                hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t waves = n < (uint32_t)max_waves ? n : (uint32_t)max_waves;
+    hipLaunchKernelGGL(k_batch_scatter, dim3((waves + 3) / 4), dim3(256), 0, stream, d_desc, n, d_stage);
+    return hipGetLastError();
+}
+
+}  // namespace cyaes

@@ -6,20 +6,26 @@
 // Rijndael pair per pipe created after the DH handshake
 // (relay_server.cpp:218-240) and deleted on close (:370-375).
 //
-// Threads: callers submit into one of kShards queues (the shard of the
-// calling thread, so a thread's requests stay in order; one short shard lock
-// per submit call, never the batcher's lock, and submit_many takes it once
-// for many requests); the builder thread closes a batch when it is full, when
-// its oldest request has waited max_delay_us, or when someone flushes -- it
-// swaps the shard queues out and forms the batch outside every lock -- gathers it into a
-// pinned staging buffer and launches H2D -> ragged encrypt -> ragged decrypt
-// -> D2H on that stage's stream; the completion thread waits for the stage,
-// scatters outputs, runs callbacks and recycles the stage.  Gather and
-// scatter of large batches are split over `workers` threads (Pool).
-// Staging layout of one batch (one H2D, one D2H):
-//   [data: each request 16-B aligned][enc meta][dec meta][key schedules]
-// A SEAL/OPEN request keeps its packet at data offset o + 4 so the payload
-// (packet offset 12) sits at o + 16.
+// Zero-copy design (round 3):
+//  * Callers register their packet memory once as pools (hipHostRegister,
+//    mapped).  A request is a 40-byte descriptor (BatchDesc) naming its input
+//    and output by device address; the GPU gathers the inputs from the pools
+//    into an HBM stage, builds SEAL packets there, runs the ragged AES kernels
+//    and scatters the outputs back into the pools (cyaes_batch_kernels.hip).
+//    The host copies no payload byte.  Requests outside every pool go through
+//    the batcher's pinned bounce buffer (host copies in and out: the legacy
+//    path, same results).
+//  * Keys: a session slot maps to a row of a device key table written once at
+//    open.  A closed row is reused only after every request enqueued before
+//    the close has completed (per-shard completion watermarks), so requests
+//    already submitted keep their key.
+//  * Submitters append descriptors to their thread's shard (one short lock per
+//    submit call); the builder swaps the shard queues out, lays the batch out
+//    with a few stores per request (encrypt-type descriptors first, then
+//    decrypt-type, so each direction is one ragged list), one H2D of the
+//    descriptors, and four kernels on the stage's stream; the completion
+//    thread waits for the stage and runs the callbacks, one job per shard on
+//    the worker pool, each shard's callbacks in its submission order.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -28,14 +34,13 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
-#include <functional>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 #include "cyaes.h"
@@ -44,49 +49,56 @@
 #include "cyaes_relay.h"
 #include "cyaes_tables.h"
 
+using cyaes::BatchDesc;
+
 namespace {
 
 using Clock = std::chrono::steady_clock;
-using Sched = std::array<uint32_t, cyaes::kSchedWords>;  // device-format schedule (cyaes_internal.h)
 
 uint64_t up16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
-
-struct Req {
-    uint8_t op;
-    std::shared_ptr<const Sched> key;  // pinned at submit: a later close/reopen does not affect it
-    const uint8_t* in;
-    uint8_t* out;
-    uint32_t size;      // ENC/DEC: bytes; SEAL: chunk bytes; OPEN: packet bytes
-    uint32_t crypt;     // bytes the kernel processes
-    int32_t conn;       // SEAL: RelayForwardMsg::id
-    cyaes_done_fn done;
-    void* user;
-    Clock::time_point t;
-    uint64_t seq;       // 1-based position in its shard's queue (flush watermark)
-    uint8_t shard;
-    uint64_t data_bytes() const { return up16(op >= CYAES_OP_RELAY_SEAL ? 16 + crypt : size); }
-};
-
-struct Stage {
-    uint8_t* h = nullptr;  // pinned
-    uint8_t* d = nullptr;  // device
-    uint64_t cap = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;
-    std::vector<Req> reqs;
-    std::vector<uint64_t> off;  // data offset per request
-    uint64_t data_end = 0;
-    int status = CYAES_OK;
-};
 
 int map_err(hipError_t e) {
     if (e == hipSuccess) return CYAES_OK;
     return (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? CYAES_ENOMEM : CYAES_EDEVICE;
 }
 
-// Fixed worker threads for the gather / scatter copies of one stage: run(n, fn)
-// calls fn(begin, end) over [0, n) in chunks, on the workers and the caller,
-// and returns when all chunks are done.  One job at a time per pool.
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
+
+constexpr int kShards = 16;            // submission shards (a thread's shard is fixed)
+constexpr uint32_t kMaxReqs = 65536;   // requests per batch
+constexpr int kMaxPools = 64;
+constexpr uint32_t kNoRow = ~0u;
+constexpr uint32_t kSchedBytes = cyaes::kSchedWords * 4;
+
+// Stage bytes of a request's data in HBM: relay packets keep their payload at
+// stage + 16 (16-B aligned), with the packet's 12 header bytes before it.
+uint64_t stage_bytes(const BatchDesc& d) { return up16(d.op >= cyaes::kOpRelaySeal ? 16 + d.crypt : d.size); }
+// Bounce bytes of a request outside the pools: one region for input and output.
+uint64_t bounce_bytes(const BatchDesc& d) {
+    switch (d.op) {
+        case cyaes::kOpRelaySeal: return up16(CYAES_RELAY_PAYLOAD_OFFSET + d.crypt);  // chunk in, packet out
+        default: return up16(d.size);                                                 // data / packet
+    }
+}
+
+struct Cb {
+    cyaes_done_fn done;
+    void* user;
+};
+
+// A queued request.  d.src / d.dst are device addresses for pooled requests;
+// for a bounced one they are the caller's host pointers until the builder
+// moves the request into a stage's bounce buffer.
+struct Pend {
+    BatchDesc d;
+    Cb cb;
+    bool bounce;
+};
+
+// Fixed worker threads: run(n, fn) calls fn(i) for i in [0, n) on the workers
+// and the caller, and returns when all are done.  One job at a time.
 class Pool {
   public:
     explicit Pool(int workers) {
@@ -100,35 +112,32 @@ class Pool {
         cv_.notify_all();
         for (auto& t : th_) t.join();
     }
-    template <typename F>
-    void run(size_t n, size_t chunk, F&& f) {
-        if (th_.empty() || n <= chunk) {
-            f(0, n);
+    void run(size_t n, const std::function<void(size_t)>& fn) {
+        if (th_.empty() || n <= 1) {
+            for (size_t i = 0; i < n; i++) fn(i);
             return;
         }
-        std::function<void(size_t, size_t)> fn(std::forward<F>(f));
         {
             std::lock_guard<std::mutex> lk(mu_);
             fn_ = &fn;
             n_ = n;
-            chunk_ = chunk;
             next_.store(0);
             active_ = (int)th_.size();
             gen_++;
         }
         cv_.notify_all();
-        work(fn, n, chunk);
+        work(fn, n);
         std::unique_lock<std::mutex> lk(mu_);
         cv_done_.wait(lk, [&] { return active_ == 0; });
         fn_ = nullptr;
     }
 
   private:
-    void work(const std::function<void(size_t, size_t)>& fn, size_t n, size_t chunk) {
+    void work(const std::function<void(size_t)>& fn, size_t n) {
         for (;;) {
-            const size_t b = next_.fetch_add(chunk);
-            if (b >= n) return;
-            fn(b, std::min(n, b + chunk));
+            const size_t i = next_.fetch_add(1);
+            if (i >= n) return;
+            fn(i);
         }
     }
     void loop() {
@@ -139,9 +148,9 @@ class Pool {
             if (stop_) return;
             seen = gen_;
             const auto* fn = fn_;
-            const size_t n = n_, chunk = chunk_;
+            const size_t n = n_;
             lk.unlock();
-            work(*fn, n, chunk);
+            work(*fn, n);
             lk.lock();
             if (--active_ == 0) cv_done_.notify_all();
         }
@@ -149,49 +158,83 @@ class Pool {
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, cv_done_;
-    const std::function<void(size_t, size_t)>* fn_ = nullptr;
-    size_t n_ = 0, chunk_ = 0;
+    const std::function<void(size_t)>* fn_ = nullptr;
+    size_t n_ = 0;
     std::atomic<size_t> next_{0};
     int active_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
 };
 
-// Requests per gather/scatter chunk: splitting pays only for large batches.
-constexpr size_t kCopyChunk = 64;
-
-// Submission shards: with one queue and one lock, 8 relay-style threads
-// resubmitting ~1 M requests/s convoyed on the lock (tools/bench_batcher.cpp).
-constexpr int kShards = 16;
 struct alignas(64) Shard {
     std::mutex mu;
-    std::vector<Req> q;
-    uint64_t bytes = 0;     // data bytes queued in q
-    uint64_t enqueued = 0;  // requests ever enqueued here (flush target, stats)
+    std::vector<Pend> q;
+    uint64_t bytes = 0;     // stage bytes queued in q
+    uint64_t enqueued = 0;  // requests ever enqueued here (flush targets, key-row stamps, stats)
 };
 int my_shard() {
     static std::atomic<int> next{0};
     thread_local int s = next.fetch_add(1) % kShards;
     return s;
 }
-// Per-thread snapshot of a batcher's session table, refreshed when the table's
-// version changes (open/close), so a submit takes no shared lock.
-std::atomic<uint64_t> g_batcher_ids{1};
-struct SessionSnap {
-    uint64_t batcher = 0, version = 0;
-    std::vector<std::shared_ptr<const Sched>> s;
+
+struct PoolEnt {
+    uint8_t* host = nullptr;
+    uint64_t dev = 0;
+    uint64_t bytes = 0;
+    bool live = false, owned = false;  // owned: registered by us (unregister on removal)
+    uint8_t* pinned = nullptr;         // the page-aligned start we registered
 };
-thread_local SessionSnap t_snap;
 
-int64_t now_ns() {
-    return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
-}
+// Per-thread snapshot of a batcher's session rows and pools, refreshed when
+// either table's version changes, so a submit takes no shared lock.
+std::atomic<uint64_t> g_batcher_ids{1};
+struct Snap {
+    uint64_t batcher = 0, sver = 0, pver = 0;
+    std::vector<uint32_t> rows;  // slot -> key row (kNoRow: closed)
+    struct Range {
+        uintptr_t lo, hi;
+        uint64_t dev;
+    };
+    std::vector<Range> pools;    // live pools by host address
+    std::vector<PoolEnt> by_id;  // pool id -> entry (cyaes_batcher_submit_pooled)
+};
+thread_local Snap t_snap;
 
-// Per-thread phase times (ns), written only by their own thread, printed by
-// cyaes_batcher_destroy when CYAES_BATCHER_PROFILE is set (after the joins).
-struct Phases {
-    int64_t wait = 0, take = 0, form = 0, layout = 0, gather = 0, submit = 0;  // builder
-    int64_t sync = 0, scatter = 0, callbacks = 0, batches = 0, reqs = 0;       // completer
+struct Seg {  // a shard's run of callbacks inside one batch
+    uint8_t shard;
+    uint32_t begin, end;  // into Stage::cbs
+    uint64_t last_seq;    // that shard's sequence number of its last request here
+};
+struct BounceOut {  // completer copy of a bounced request's output
+    uint8_t* to;
+    const uint8_t* from;
+    uint32_t bytes;
+};
+
+struct Stage {
+    BatchDesc* h_enc = nullptr;  // pinned: encrypt-type descriptors [0, kMaxReqs)
+    BatchDesc* h_dec = nullptr;  // pinned: decrypt-type descriptors [0, kMaxReqs)
+    uint8_t* h_bounce = nullptr; // pinned, mapped
+    uint64_t bounce_dev = 0;
+    uint8_t* d_mem = nullptr;    // device: descriptors | lists | data
+    BatchDesc* d_desc = nullptr;
+    uint64_t* d_offs = nullptr;
+    uint32_t *d_nb = nullptr, *d_kid = nullptr;
+    uint8_t* d_data = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint32_t ne = 0, nd = 0;
+    uint64_t bytes = 0;  // payload bytes en/decrypted (stats)
+    std::vector<Cb> cbs;
+    std::vector<Seg> segs;
+    std::vector<BounceOut> bouts;
+    int status = CYAES_OK;
+};
+
+struct Phases {  // per-batch phase times (ns), CYAES_BATCHER_PROFILE
+    int64_t wait = 0, take = 0, layout = 0, copy_in = 0, submit = 0;
+    int64_t sync = 0, copy_out = 0, callbacks = 0, batches = 0, reqs = 0;
 };
 
 }  // namespace
@@ -199,76 +242,213 @@ struct Phases {
 struct cyaes_batcher {
     cyaes_batcher_config cfg{};
     cyaes_gpu* ctx = nullptr;
-    uint64_t stage_cap = 0;
+    uint64_t data_cap = 0, bounce_cap = 0;
+    int gather_waves = 0;
     std::vector<Stage> stages;
 
-    // Submission: shard queues + counters (lock-free for submitters except their shard).
     std::array<Shard, kShards> shards;
-    std::atomic<int64_t> queued_reqs{0}, queued_bytes{0};  // transiently negative while a drain races an enqueue
-    std::atomic<int64_t> oldest_ns{0};  // submit time of the oldest queued request (0: none recorded)
+    std::atomic<int64_t> queued_reqs{0}, queued_bytes{0};
+    std::atomic<int64_t> oldest_ns{0};
     std::atomic<int> flushers{0};
     std::atomic<bool> stop{false};
 
-    // Builder / completion hand-off, stats, flush (guarded by mu).
-    std::mutex mu;
+    std::mutex mu;  // builder / completer hand-off, stats, flush
     std::condition_variable cv_submit, cv_free, cv_inflight, cv_flush;
     std::vector<Stage*> free_stages;
     std::deque<Stage*> inflight;
     bool builder_done = false;
-    uint64_t completed = 0;
-    // Per-shard completion watermark: the highest seq completed.  A shard's
-    // requests complete in enqueue order (the builder appends each shard's
-    // queue to carry in order, cuts batches in carry order, and batches
-    // complete in launch order), so flush waits for every shard's watermark to
-    // reach that shard's count at the call -- a global count could be reached
-    // by later requests of other shards while earlier ones are still queued.
-    std::array<uint64_t, kShards> done_seq{};
-    uint64_t batches = 0, bytes = 0, max_batch = 0, errors = 0;
+    uint64_t completed = 0, batches = 0, bytes = 0, max_batch = 0, errors = 0;
     int first_error = CYAES_OK;
+    std::array<uint64_t, kShards> done_seq{};  // per shard: requests completed (they complete in order)
 
-    std::mutex smu;  // session table
-    std::vector<std::shared_ptr<const Sched>> sessions;  // nullptr = free slot
+    // Sessions: slot -> device key-table row.
+    std::mutex smu;
+    uint32_t key_cap = 0;
+    uint32_t* d_keys = nullptr;
+    std::vector<uint32_t> slot_row;
+    std::vector<uint32_t> free_rows;
+    uint32_t next_row = 0;
+    struct Retired {
+        uint32_t row;
+        std::array<uint64_t, kShards> stamp;  // shard enqueue counts at the close
+    };
+    std::vector<Retired> retired;
     std::atomic<uint64_t> sessions_version{1};
+
+    // Pools.
+    std::mutex pmu;
+    std::array<PoolEnt, kMaxPools> pools{};
+    std::atomic<uint64_t> pools_version{1};
+
     const uint64_t id = g_batcher_ids.fetch_add(1);
-    const SessionSnap& snapshot();
-    uint64_t enqueued_total();
-
-    std::unique_ptr<Pool> gather_pool, scatter_pool;
+    std::unique_ptr<Pool> workers;  // bounce copies, callbacks
     std::thread builder, completer;
-    Phases pb, pc;  // builder / completer phase times
-    struct Lists {  // builder-private scratch of launch(), reused across batches
-        std::vector<uint64_t> eo, doff, o2;
-        std::vector<uint32_t> el, ek, dl, dk, l2, k2, at;
-        std::unordered_map<const Sched*, uint32_t> kidx;
-        std::vector<const Sched*> klist;
-    } lists;
+    Phases pb, pc;
 
-    // Cost of a request in a stage: data + meta (16 B) + a schedule if its key is new to the batch.
-    static uint64_t cost(const Req& r) { return r.data_bytes() + 16; }
-
+    const Snap& snapshot();
+    int make(const cyaes_batch_req& q, const Snap& ss, Pend* p);
+    int make_pooled(const cyaes_pool_req& q, const Snap& ss, Pend* p);
+    template <typename MakeAll>
+    int enqueue(MakeAll&& make_all);
     void build_loop();
     void complete_loop();
     int launch(Stage* st);
-    int make(const cyaes_batch_req& q, const SessionSnap& ss, Req* r);
-    void enqueue(Req* rs, size_t n, uint64_t nbytes);
+    int wait_enqueued(const std::array<uint64_t, kShards>& target);
 };
 
+// ---- submission --------------------------------------------------------------
+const Snap& cyaes_batcher::snapshot() {
+    Snap& ss = t_snap;
+    const uint64_t sv = sessions_version.load(std::memory_order_acquire);
+    const uint64_t pv = pools_version.load(std::memory_order_acquire);
+    if (ss.batcher != id || ss.sver != sv) {
+        std::lock_guard<std::mutex> lk(smu);
+        ss.rows = slot_row;
+        ss.sver = sessions_version.load(std::memory_order_relaxed);
+    }
+    if (ss.batcher != id || ss.pver != pv) {
+        std::lock_guard<std::mutex> lk(pmu);
+        ss.pools.clear();
+        ss.by_id.assign(pools.begin(), pools.end());
+        for (const PoolEnt& e : pools)
+            if (e.live) ss.pools.push_back({(uintptr_t)e.host, (uintptr_t)e.host + e.bytes, e.dev});
+        std::sort(ss.pools.begin(), ss.pools.end(), [](const Snap::Range& a, const Snap::Range& b) { return a.lo < b.lo; });
+        ss.pver = pools_version.load(std::memory_order_relaxed);
+    }
+    ss.batcher = id;
+    return ss;
+}
+
+// Device address of host range [p, p + n) if a registered pool holds all of it, else 0.
+static uint64_t pool_dev(const Snap& ss, const void* p, uint64_t n) {
+    const uintptr_t a = (uintptr_t)p;
+    auto it = std::upper_bound(ss.pools.begin(), ss.pools.end(), a,
+                               [](uintptr_t x, const Snap::Range& r) { return x < r.lo; });
+    if (it == ss.pools.begin()) return 0;
+    --it;
+    if (a < it->lo || a + n > it->hi || a + n < a) return 0;
+    return it->dev + (a - it->lo);
+}
+
+// Validates one pointer request; finds its pools (or marks it bounced).
+int cyaes_batcher::make(const cyaes_batch_req& q, const Snap& ss, Pend* p) {
+    *p = Pend{};
+    BatchDesc& d = p->d;
+    const uint8_t *in = nullptr, *out = nullptr;
+    uint64_t in_n = 0, out_n = 0;
+    switch (q.op) {
+        case CYAES_OP_ENCRYPT:
+        case CYAES_OP_DECRYPT:
+            if (q.size % 16 || q.size > cfg.max_batch_bytes || (q.size && (!q.in || !q.out))) return CYAES_EINVAL;
+            d.size = d.crypt = q.size;
+            in = q.in, out = q.out, in_n = out_n = q.size;
+            break;
+        case CYAES_OP_RELAY_SEAL:
+            if (!q.out || q.size > CYAES_RELAY_MAX_CHUNK || (q.size && !q.in)) return CYAES_EINVAL;
+            d.size = q.size;
+            d.crypt = cyaes_relay_round16(q.size);
+            d.conn = q.conn_id;
+            in = q.in, out = q.out, in_n = q.size, out_n = CYAES_RELAY_PAYLOAD_OFFSET + d.crypt;
+            break;
+        case CYAES_OP_RELAY_OPEN: {
+            uint8_t* packet = q.out ? q.out : const_cast<uint8_t*>(q.in);
+            if (!packet || q.size < CYAES_RELAY_PAYLOAD_OFFSET) return CYAES_EINVAL;
+            const uint32_t psize = (uint32_t)((packet[0] << 8) | packet[1]);  // BE u16 (cye_packet.cpp:82-86)
+            const uint32_t pid = (uint32_t)((packet[2] << 8) | packet[3]);
+            if (pid != CYAES_RELAY_FORWARD || psize + CYAES_RELAY_HEADSIZE != q.size || psize < 8 || (psize - 8) % 16)
+                return CYAES_EINVAL;
+            d.size = q.size;
+            d.crypt = psize - 8u;  // relay_server.cpp:329: packet_size - sizeof(RelayForwardMsg)
+            in = out = packet, in_n = out_n = q.size;
+            break;
+        }
+        default:
+            return CYAES_EINVAL;
+    }
+    if (q.slot >= ss.rows.size() || ss.rows[q.slot] == kNoRow) return CYAES_ERANGE;
+    d.op = (uint32_t)q.op;
+    d.key = ss.rows[q.slot];
+    p->cb = Cb{q.done, q.user};
+    const uint64_t ds = in_n ? pool_dev(ss, in, in_n) : 1, dd = out_n ? pool_dev(ss, out, out_n) : 1;
+    if (ds && dd) {  // zero-copy: the GPU reads and writes the caller's pool memory itself
+        d.src = in_n ? ds : 0;
+        d.dst = out_n ? dd : 0;
+    } else {
+        p->bounce = true;
+        d.src = (uint64_t)(uintptr_t)in;
+        d.dst = (uint64_t)(uintptr_t)out;
+    }
+    return CYAES_OK;
+}
+
+int cyaes_batcher::make_pooled(const cyaes_pool_req& q, const Snap& ss, Pend* p) {
+    if (q.pool >= ss.by_id.size() || !ss.by_id[q.pool].live) return CYAES_EINVAL;
+    const PoolEnt& e = ss.by_id[q.pool];
+    if (q.in_off > e.bytes || (q.op != CYAES_OP_RELAY_OPEN && q.out_off > e.bytes)) return CYAES_EINVAL;
+    cyaes_batch_req r{q.op, q.slot, q.conn_id, e.host + q.in_off,
+                      q.op == CYAES_OP_RELAY_OPEN ? e.host + q.in_off : e.host + q.out_off, q.size, q.done, q.user};
+    const int st = make(r, ss, p);
+    if (st == CYAES_OK && p->bounce) return CYAES_EINVAL;  // the request runs past its pool's end
+    return st;
+}
+
+// Builds this thread's requests against its snapshot and appends them to its
+// shard under one lock.  The snapshot is re-checked under the shard lock: a
+// close stamps its key row with the shard counts (taking each shard lock), so
+// a request either enqueued before that stamp (and keeps the row alive) or
+// sees the new version and is rebuilt against it (ERANGE for a closed slot).
+template <typename MakeAll>
+int cyaes_batcher::enqueue(MakeAll&& make_all) {
+    thread_local std::vector<Pend> ps;
+    const int s = my_shard();
+    Shard& sh = shards[s];
+    for (;;) {
+        const Snap& ss = snapshot();
+        ps.clear();
+        uint64_t nbytes = 0;
+        const int first = make_all(ss, ps, nbytes);
+        if (ps.empty()) return first;
+        int64_t before, b0;
+        {
+            std::lock_guard<std::mutex> lk(sh.mu);
+            if (sessions_version.load(std::memory_order_acquire) != ss.sver ||
+                pools_version.load(std::memory_order_acquire) != ss.pver)
+                continue;  // a session or pool changed since the snapshot: rebuild
+            sh.q.insert(sh.q.end(), ps.begin(), ps.end());
+            sh.bytes += nbytes;
+            sh.enqueued += ps.size();
+        }
+        if (oldest_ns.load(std::memory_order_relaxed) == 0) {
+            int64_t zero = 0;
+            oldest_ns.compare_exchange_strong(zero, now_ns());
+        }
+        before = queued_reqs.fetch_add((int64_t)ps.size());
+        b0 = queued_bytes.fetch_add((int64_t)nbytes);
+        const int64_t cap = cfg.max_batch_bytes;
+        if (before <= 0 || (b0 < cap && b0 + (int64_t)nbytes >= cap)) {
+            std::lock_guard<std::mutex> lk(mu);  // orders the wake-up after the builder's predicate check
+            cv_submit.notify_one();
+        }
+        return first;
+    }
+}
+
+// ---- builder ---------------------------------------------------------------
 void cyaes_batcher::build_loop() {
-    std::vector<Req> carry;  // builder-private: taken from the shards, not yet batched (older than the shards)
-    size_t cpos = 0;
-    std::array<std::vector<Req>, kShards> spare;  // swapped into the shards: their capacity is recycled
-    std::unordered_map<const Sched*, int> seen;
+    std::array<std::vector<Pend>, kShards> pend, spare;  // builder-private: taken, not yet batched
+    std::array<size_t, kShards> ppos{};
+    std::array<uint64_t, kShards> batched{};  // per shard: requests put into batches so far
+    int rr = 0;
     for (;;) {
         Stage* st = nullptr;
         const int64_t tw = now_ns();
+        bool have = false;
+        for (int s = 0; s < kShards && !have; s++) have = ppos[s] < pend[s].size();
         {
             std::unique_lock<std::mutex> lk(mu);
-            if (cpos == carry.size()) {
-                carry.clear();
-                cpos = 0;
+            if (!have) {
                 cv_submit.wait(lk, [&] { return stop || queued_reqs.load() > 0; });
                 if (queued_reqs.load() <= 0) break;  // stop requested and drained
-                // Let the batch fill: until it is full, the oldest request is due, or a flush/stop.
                 const int64_t t = oldest_ns.load();
                 const auto due = Clock::time_point(std::chrono::nanoseconds(t ? t : now_ns())) +
                                  std::chrono::microseconds(cfg.max_delay_us);
@@ -282,68 +462,105 @@ void cyaes_batcher::build_loop() {
         }
         const int64_t tt = now_ns();
         pb.wait += tt - tw;
-        // Take every shard's queue: a swap with a spare (empty, with capacity)
-        // under each shard lock, then one move per request into carry.
         oldest_ns.store(0);
         int64_t took = 0, took_bytes = 0;
-        for (int i = 0; i < kShards; i++) {
-            Shard& sh = shards[i];
+        for (int s = 0; s < kShards; s++) {
+            Shard& sh = shards[s];
             {
                 std::lock_guard<std::mutex> lk(sh.mu);
                 if (sh.q.empty()) continue;
-                sh.q.swap(spare[i]);
+                sh.q.swap(spare[s]);
                 took_bytes += (int64_t)sh.bytes;
                 sh.bytes = 0;
             }
-            std::vector<Req>& q = spare[i];
-            took += (int64_t)q.size();
-            if (cpos == carry.size()) {
-                carry.clear();
-                cpos = 0;
+            took += (int64_t)spare[s].size();
+            if (ppos[s] == pend[s].size()) {
+                pend[s].clear();
+                ppos[s] = 0;
             }
-            if (carry.empty()) carry.swap(q);  // q now holds carry's old (empty) buffer
-            else carry.insert(carry.end(), std::make_move_iterator(q.begin()), std::make_move_iterator(q.end()));
-            q.clear();
+            if (pend[s].empty()) pend[s].swap(spare[s]);
+            else pend[s].insert(pend[s].end(), spare[s].begin(), spare[s].end());
+            spare[s].clear();
         }
         queued_reqs.fetch_sub(took);
         queued_bytes.fetch_sub(took_bytes);
-        const int64_t tf = now_ns();
-        pb.take += tf - tt;
-        // Cut the batch: [cpos, end) of carry, bounded by max_batch_bytes and the stage.
-        st->reqs.clear();
-        uint64_t used = 0, data = 0;
-        seen.clear();
-        const Sched* last = nullptr;
-        size_t end = cpos;
-        for (; end < carry.size(); end++) {
-            const Req& r = carry[end];
-            bool new_key = false;
-            if (r.key.get() != last) {
-                last = r.key.get();
-                new_key = seen.emplace(last, 0).second;
+        const int64_t tl = now_ns();
+        pb.take += tl - tt;
+
+        // Lay the batch out: shards in rotating order, each shard's requests in
+        // submission order, until the stage's requests, data or bounce is full.
+        st->ne = st->nd = 0;
+        st->bytes = 0;
+        st->cbs.clear();
+        st->segs.clear();
+        st->bouts.clear();
+        uint64_t data = 0, bounce = 0;
+        bool full = false;
+        thread_local std::vector<std::array<const uint8_t*, 3>> copies;  // (to, from, bytes) bounce inputs
+        copies.clear();
+        for (int k = 0; k < kShards && !full; k++) {
+            const int s = (rr + k) % kShards;
+            std::vector<Pend>& q = pend[s];
+            const uint32_t cb0 = (uint32_t)st->cbs.size();
+            size_t i = ppos[s];
+            for (; i < q.size(); i++) {
+                Pend& p = q[i];
+                const uint64_t sb = stage_bytes(p.d), bb = p.bounce ? bounce_bytes(p.d) : 0;
+                // (the first request of a batch always fits: submit caps a request's size)
+                if (st->ne + st->nd > 0 &&
+                    (st->ne + st->nd == kMaxReqs || data + sb > data_cap || bounce + bb > bounce_cap)) {
+                    full = true;
+                    break;
+                }
+                BatchDesc d = p.d;
+                d.stage = (uint32_t)data;
+                data += sb;
+                if (p.bounce) {  // through the pinned bounce buffer: in now, out at completion
+                    uint8_t* hb = st->h_bounce + bounce;
+                    const uint8_t* in = reinterpret_cast<const uint8_t*>((uintptr_t)p.d.src);
+                    uint8_t* out = reinterpret_cast<uint8_t*>((uintptr_t)p.d.dst);
+                    const uint32_t in_n = d.size;  // ENC/DEC data, SEAL chunk, OPEN packet
+                    if (in_n) copies.push_back({hb, in, reinterpret_cast<const uint8_t*>((uintptr_t)in_n)});
+                    d.src = d.dst = st->bounce_dev + bounce;
+                    switch (d.op) {
+                        case cyaes::kOpRelaySeal:
+                            st->bouts.push_back({out, hb, CYAES_RELAY_PAYLOAD_OFFSET + d.crypt});
+                            break;
+                        case cyaes::kOpRelayOpen:
+                            st->bouts.push_back({out + CYAES_RELAY_PAYLOAD_OFFSET, hb + CYAES_RELAY_PAYLOAD_OFFSET, d.crypt});
+                            break;
+                        default:
+                            if (d.size) st->bouts.push_back({out, hb, d.size});
+                    }
+                    bounce += bb;
+                }
+                if (d.op == cyaes::kOpEncrypt || d.op == cyaes::kOpRelaySeal) st->h_enc[st->ne++] = d;
+                else st->h_dec[st->nd++] = d;
+                st->cbs.push_back(p.cb);
+                st->bytes += d.crypt;
             }
-            const uint64_t db = r.data_bytes();
-            const uint64_t c = db + 16 + (new_key ? sizeof(Sched) : 0);
-            if (end > cpos && (data + db > cfg.max_batch_bytes || used + c + 64 > stage_cap)) break;
-            used += c;
-            data += db;
+            const uint32_t taken = (uint32_t)(i - ppos[s]);
+            if (taken) {
+                batched[s] += taken;
+                st->segs.push_back({(uint8_t)s, cb0, (uint32_t)st->cbs.size(), batched[s]});
+            }
+            ppos[s] = i;
         }
-        if (cpos == 0 && end == carry.size()) {
-            st->reqs.swap(carry);  // the whole carry: no moves (carry takes the stage's old buffer)
-            carry.clear();
-            cpos = 0;
-        } else {
-            st->reqs.insert(st->reqs.end(), std::make_move_iterator(carry.begin() + cpos),
-                            std::make_move_iterator(carry.begin() + end));
-            cpos = end;
-        }
-        if (st->reqs.empty()) {  // raced: nothing taken (cannot happen with took > 0 or carry)
+        rr = (rr + 1) % kShards;
+        const int64_t tc = now_ns();
+        pb.layout += tc - tl;
+        if (st->cbs.empty()) {  // nothing taken (raced)
             std::lock_guard<std::mutex> lk(mu);
             free_stages.push_back(st);
             continue;
         }
-        pb.form += now_ns() - tf;
+        workers->run(copies.size(), [&](size_t i) {
+            memcpy(const_cast<uint8_t*>(copies[i][0]), copies[i][1], (size_t)(uintptr_t)copies[i][2]);
+        });
+        const int64_t ts = now_ns();
+        pb.copy_in += ts - tc;
         st->status = launch(st);
+        pb.submit += now_ns() - ts;
         std::lock_guard<std::mutex> lk(mu);
         inflight.push_back(st);
         cv_inflight.notify_one();
@@ -353,166 +570,32 @@ void cyaes_batcher::build_loop() {
     cv_inflight.notify_all();
 }
 
-// Gathers st->reqs into the stage and launches the batch on its stream.
+// One H2D of the descriptors, then gather -> encrypt -> decrypt -> scatter on
+// the stage's stream (cyaes_batch_kernels.hip, cyaes_kernels.hip).
 int cyaes_batcher::launch(Stage* st) {
-    const int64_t t0 = now_ns();
-    const size_t n = st->reqs.size();
-    st->off.resize(n);
-    // Data section + per-direction lists.
-    std::vector<uint64_t>& eo = lists.eo;
-    std::vector<uint64_t>& doff = lists.doff;
-    std::vector<uint32_t>&el = lists.el, &ek = lists.ek, &dl = lists.dl, &dk = lists.dk;
-    for (auto* v : {&eo, &doff}) v->clear(), v->reserve(n);
-    for (auto* v : {&el, &ek, &dl, &dk}) v->clear(), v->reserve(n);
-    std::unordered_map<const Sched*, uint32_t>& kidx = lists.kidx;
-    std::vector<const Sched*>& klist = lists.klist;
-    kidx.clear();
-    klist.clear();
-    const Sched* last = nullptr;
-    uint32_t k = 0;
-    uint64_t pos = 0;
-    for (size_t i = 0; i < n; i++) {  // layout pass (the copies run below, in parallel)
-        const Req& r = st->reqs[i];
-        st->off[i] = pos;
-        const uint64_t coff = r.op >= CYAES_OP_RELAY_SEAL ? pos + 16 : pos;  // where the kernel works
-        pos += r.data_bytes();
-        if (r.crypt == 0) continue;  // size 0: a no-op (cyr_rijndael.cpp:600 loop never runs)
-        if (r.key.get() != last) {  // requests come in per-thread runs: hash only on a change
-            last = r.key.get();
-            auto it = kidx.find(last);
-            if (it == kidx.end()) {
-                k = (uint32_t)klist.size();
-                kidx.emplace(last, k);
-                klist.push_back(last);
-            } else {
-                k = it->second;
-            }
-        }
-        const bool dec = r.op == CYAES_OP_DECRYPT || r.op == CYAES_OP_RELAY_OPEN;
-        (dec ? doff : eo).push_back(coff);
-        (dec ? dl : el).push_back(r.crypt);
-        (dec ? dk : ek).push_back(k);
-    }
-    st->data_end = pos;
-    const int64_t t1 = now_ns();
-    pb.layout += t1 - t0;
-    gather_pool->run(n, kCopyChunk, [st](size_t b, size_t e) {
-        for (size_t i = b; i < e; i++) {
-            const Req& r = st->reqs[i];
-            uint8_t* dst = st->h + st->off[i];
-            switch (r.op) {
-                case CYAES_OP_ENCRYPT:
-                case CYAES_OP_DECRYPT:
-                    memcpy(dst, r.in, r.size);
-                    break;
-                case CYAES_OP_RELAY_SEAL:  // relay_local.cpp:189-201: packet build + 0xCE padding
-                    cyaes_relay_build_forward(dst + 4, r.conn, r.in, r.size);
-                    break;
-                case CYAES_OP_RELAY_OPEN:
-                    memcpy(dst + 4, r.in, r.size);
-                    break;
-            }
-        }
-    });
-    const int64_t t2 = now_ns();
-    pb.gather += t2 - t1;
-    // Encrypt runs one chain per lane and waterfalls over the distinct keys of
-    // a wave (cyaes_kernels.hip, k_encrypt), so order its list by key: a wave
-    // then sees one key, two at a boundary, instead of one per looper thread.
-    // (Decrypt runs one payload per wave: one key per wave already.)
-    // (Only for the lane-per-chain kernel: below its threshold the ragged
-    // encrypt runs four lanes per chain with per-chain keys, and order does
-    // not matter.)
-    if (klist.size() > 1 && !eo.empty() && !cyaes::ragged_encrypt_is_quad(ctx, eo.size())) {
-        // Stable counting sort by key index (key indices are dense: 0..klist.size()-1).
-        std::vector<uint64_t>& o2 = lists.o2;
-        std::vector<uint32_t>&l2 = lists.l2, &k2 = lists.k2, &at = lists.at;
-        o2.resize(eo.size());
-        l2.resize(el.size());
-        k2.resize(ek.size());
-        at.assign(klist.size() + 1, 0);
-        for (uint32_t x : ek) at[x + 1]++;
-        for (size_t j = 1; j < at.size(); j++) at[j] += at[j - 1];
-        for (size_t i = 0; i < ek.size(); i++) {
-            const uint32_t d = at[ek[i]]++;
-            o2[d] = eo[i], l2[d] = el[i], k2[d] = ek[i];
-        }
-        // Small batch: start every key group on a wave boundary with empty
-        // (0-byte) lanes, so no wave waterfalls; the waves are then all
-        // latency-bound chains on separate CUs (A/B on bench_batcher seal 1472 B).
-        uint64_t waves = 0;
-        for (size_t i = 0; i < k2.size();) {
-            size_t j = i;
-            while (j < k2.size() && k2[j] == k2[i]) j++;
-            waves += (j - i + 63) / 64;
-            i = j;
-        }
-        if (waves <= 4096) {
-            eo.clear(), el.clear(), ek.clear();
-            for (size_t i = 0; i < k2.size(); i++) {
-                if (i && k2[i] != k2[i - 1])
-                    while (eo.size() % 64) eo.push_back(0), el.push_back(0), ek.push_back(k2[i - 1]);
-                eo.push_back(o2[i]), el.push_back(l2[i]), ek.push_back(k2[i]);
-            }
-        } else {
-            eo.swap(o2);
-            el.swap(l2);
-            ek.swap(k2);
-        }
-    }
-    // Meta + keys after the data.
-    auto put = [&](const void* src, size_t bytes) {
-        const uint64_t at = pos;
-        if (bytes) memcpy(st->h + at, src, bytes);
-        pos = up16(pos + bytes);
-        return at;
-    };
-    const uint64_t eo_at = put(eo.data(), eo.size() * 8), el_at = put(el.data(), el.size() * 4),
-                   ek_at = put(ek.data(), ek.size() * 4);
-    const uint64_t do_at = put(doff.data(), doff.size() * 8), dl_at = put(dl.data(), dl.size() * 4),
-                   dk_at = put(dk.data(), dk.size() * 4);
-    const uint64_t keys_at = pos;
-    for (const Sched* s : klist) put(s->data(), sizeof(Sched));
-    if (pos > st->cap) return CYAES_ENOMEM;  // cannot happen: cost() bounds it
-
-    hipError_t e = hipMemcpyAsync(st->d, st->h, pos, hipMemcpyHostToDevice, st->stream);
+    const uint32_t ne = st->ne, nd = st->nd, n = ne + nd;
+    hipError_t e = hipSuccess;
+    if (ne) e = hipMemcpyAsync(st->d_desc, st->h_enc, ne * sizeof(BatchDesc), hipMemcpyHostToDevice, st->stream);
+    if (e == hipSuccess && nd)
+        e = hipMemcpyAsync(st->d_desc + ne, st->h_dec, nd * sizeof(BatchDesc), hipMemcpyHostToDevice, st->stream);
+    if (e == hipSuccess)
+        e = cyaes::launch_batch_gather(st->d_desc, n, st->d_data, st->d_offs, st->d_nb, st->d_kid, gather_waves,
+                                       st->stream);
     if (e != hipSuccess) return map_err(e);
-    const uint32_t* table = reinterpret_cast<const uint32_t*>(st->d + keys_at);
-    const uint32_t nk = (uint32_t)klist.size();
     int rc = CYAES_OK;
-    if (!eo.empty())
-        rc = cyaes::ragged_batch(ctx, false, table, nk, st->d, st->d, reinterpret_cast<const uint64_t*>(st->d + eo_at),
-                                 reinterpret_cast<const uint32_t*>(st->d + el_at), eo.size(),
-                                 reinterpret_cast<const uint32_t*>(st->d + ek_at), st->stream);
-    if (rc == CYAES_OK && !doff.empty())
-        rc = cyaes::ragged_batch(ctx, true, table, nk, st->d, st->d, reinterpret_cast<const uint64_t*>(st->d + do_at),
-                                 reinterpret_cast<const uint32_t*>(st->d + dl_at), doff.size(),
-                                 reinterpret_cast<const uint32_t*>(st->d + dk_at), st->stream);
+    if (ne)
+        rc = cyaes::ragged_batch(ctx, false, d_keys, key_cap, st->d_data, st->d_data, st->d_offs, st->d_nb, ne,
+                                 st->d_kid, st->stream);
+    if (rc == CYAES_OK && nd)
+        rc = cyaes::ragged_batch(ctx, true, d_keys, key_cap, st->d_data, st->d_data, st->d_offs + ne, st->d_nb + ne,
+                                 nd, st->d_kid + ne, st->stream);
     if (rc != CYAES_OK) return rc;
-    e = hipMemcpyAsync(st->h, st->d, st->data_end, hipMemcpyDeviceToHost, st->stream);
+    e = cyaes::launch_batch_scatter(st->d_desc, n, st->d_data, gather_waves, st->stream);
     if (e == hipSuccess) e = hipEventRecord(st->done, st->stream);
-    pb.submit += now_ns() - t2;
     return map_err(e);
 }
 
-// Copies request i's result out of the stage into the caller's buffer.
-static void scatter(Stage* st, size_t i) {
-    const Req& r = st->reqs[i];
-    const uint8_t* src = st->h + st->off[i];
-    switch (r.op) {
-        case CYAES_OP_ENCRYPT:
-        case CYAES_OP_DECRYPT:
-            memcpy(r.out, src, r.size);
-            break;
-        case CYAES_OP_RELAY_SEAL:
-            memcpy(r.out, src + 4, CYAES_RELAY_PAYLOAD_OFFSET + r.crypt);
-            break;
-        case CYAES_OP_RELAY_OPEN:  // header untouched, payload decrypted in place
-            memcpy(r.out + CYAES_RELAY_PAYLOAD_OFFSET, src + 16, r.crypt);
-            break;
-    }
-}
-
+// ---- completion ------------------------------------------------------------
 void cyaes_batcher::complete_loop() {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
@@ -524,38 +607,33 @@ void cyaes_batcher::complete_loop() {
         int status = st->status;
         const int64_t t0 = now_ns();
         if (status == CYAES_OK) status = map_err(hipEventSynchronize(st->done));
-        // A stage whose submit failed part-way may still have copies or kernels in
-        // flight on its buffers: drain its stream before the stage is reused.
+        // A stage whose launch failed part-way may still have work in flight on
+        // its buffers: drain its stream before the stage is reused.
         if (status != CYAES_OK) (void)hipStreamSynchronize(st->stream);
         const int64_t t1 = now_ns();
         pc.sync += t1 - t0;
         if (status == CYAES_OK)
-            scatter_pool->run(st->reqs.size(), kCopyChunk, [st](size_t b, size_t e) {
-                for (size_t i = b; i < e; i++) scatter(st, i);
+            workers->run(st->bouts.size(), [st](size_t i) {
+                const BounceOut& b = st->bouts[i];
+                memcpy(b.to, b.from, b.bytes);
             });
         const int64_t t2 = now_ns();
-        pc.scatter += t2 - t1;
-        // Callbacks on this thread, in batch order.  (A/B: spreading them over
-        // the scatter workers by submission shard was slower under the
-        // relay-shaped load of tools/bench_batcher.cpp: the callbacks then
-        // contend with the submitting threads.)
-        uint64_t nbytes = 0;
-        std::array<uint64_t, kShards> hi{};
-        for (const Req& r : st->reqs) {
-            nbytes += r.crypt;
-            hi[r.shard] = std::max(hi[r.shard], r.seq);
-            if (r.done) r.done(r.user, status);
-        }
-        const size_t nreq = st->reqs.size();
-        st->reqs.clear();  // drops the schedule references
+        pc.copy_out += t2 - t1;
+        // Callbacks: one job per shard run, in that shard's submission order.
+        workers->run(st->segs.size(), [st, status](size_t k) {
+            const Seg& g = st->segs[k];
+            for (uint32_t i = g.begin; i < g.end; i++)
+                if (st->cbs[i].done) st->cbs[i].done(st->cbs[i].user, status);
+        });
+        const size_t nreq = st->cbs.size();
         pc.callbacks += now_ns() - t2;
         pc.batches++;
         pc.reqs += (int64_t)nreq;
         lk.lock();
         completed += nreq;
-        for (int i = 0; i < kShards; i++) done_seq[i] = std::max(done_seq[i], hi[i]);
+        for (const Seg& g : st->segs) done_seq[g.shard] = std::max(done_seq[g.shard], g.last_seq);
         batches++;
-        bytes += nbytes;
+        bytes += st->bytes;
         max_batch = std::max<uint64_t>(max_batch, nreq);
         if (status != CYAES_OK) {
             errors += nreq;
@@ -567,101 +645,29 @@ void cyaes_batcher::complete_loop() {
     }
 }
 
-// This thread's snapshot of the session table (refreshed under smu when an
-// open/close has bumped the version since this thread last looked).
-const SessionSnap& cyaes_batcher::snapshot() {
-    SessionSnap& ss = t_snap;
-    const uint64_t v = sessions_version.load(std::memory_order_acquire);
-    if (ss.batcher != id || ss.version != v) {
-        std::lock_guard<std::mutex> lk(smu);
-        ss.s = sessions;
-        ss.batcher = id;
-        ss.version = sessions_version.load(std::memory_order_relaxed);
-    }
-    return ss;
+// Waits until every shard has completed `target` requests (flush semantics).
+int cyaes_batcher::wait_enqueued(const std::array<uint64_t, kShards>& target) {
+    std::unique_lock<std::mutex> lk(mu);
+    flushers.fetch_add(1);
+    cv_submit.notify_all();
+    cv_flush.wait(lk, [&] {
+        for (int i = 0; i < kShards; i++)
+            if (done_seq[i] < target[i]) return false;
+        return true;
+    });
+    flushers.fetch_sub(1);
+    const int err = first_error;
+    first_error = CYAES_OK;
+    return err;
 }
 
-uint64_t cyaes_batcher::enqueued_total() {
-    uint64_t n = 0;
-    for (Shard& sh : shards) {
-        std::lock_guard<std::mutex> lk(sh.mu);
-        n += sh.enqueued;
+static std::array<uint64_t, kShards> enqueue_counts(cyaes_batcher* b) {
+    std::array<uint64_t, kShards> t;
+    for (int i = 0; i < kShards; i++) {
+        std::lock_guard<std::mutex> sl(b->shards[i].mu);
+        t[i] = b->shards[i].enqueued;
     }
-    return n;
-}
-
-// Validates one request and pins its session's schedule.
-int cyaes_batcher::make(const cyaes_batch_req& q, const SessionSnap& ss, Req* r) {
-    *r = Req{};
-    switch (q.op) {
-        case CYAES_OP_ENCRYPT:
-        case CYAES_OP_DECRYPT:
-            if (q.size % 16 || q.size > cfg.max_batch_bytes || (q.size && (!q.in || !q.out))) return CYAES_EINVAL;
-            r->size = r->crypt = q.size;
-            r->in = q.in;
-            r->out = q.out;
-            break;
-        case CYAES_OP_RELAY_SEAL:
-            if (!q.out || q.size > CYAES_RELAY_MAX_CHUNK || (q.size && !q.in)) return CYAES_EINVAL;
-            r->in = q.in;
-            r->out = q.out;
-            r->size = q.size;
-            r->crypt = cyaes_relay_round16(q.size);
-            r->conn = q.conn_id;
-            break;
-        case CYAES_OP_RELAY_OPEN: {
-            uint8_t* packet = q.out ? q.out : const_cast<uint8_t*>(q.in);
-            if (!packet || q.size < CYAES_RELAY_PAYLOAD_OFFSET) return CYAES_EINVAL;
-            const uint32_t psize = (uint32_t)((packet[0] << 8) | packet[1]);  // BE u16 (cye_packet.cpp:82-86)
-            const uint32_t pid = (uint32_t)((packet[2] << 8) | packet[3]);
-            if (pid != CYAES_RELAY_FORWARD || psize + CYAES_RELAY_HEADSIZE != q.size || psize < 8 || (psize - 8) % 16)
-                return CYAES_EINVAL;
-            r->in = packet;
-            r->out = packet;
-            r->size = q.size;
-            r->crypt = psize - 8u;  // relay_server.cpp:329: packet_size - sizeof(RelayForwardMsg)
-            break;
-        }
-        default:
-            return CYAES_EINVAL;
-    }
-    if (q.slot >= ss.s.size() || !ss.s[q.slot]) return CYAES_ERANGE;
-    r->op = (uint8_t)q.op;
-    r->key = ss.s[q.slot];
-    r->done = q.done;
-    r->user = q.user;
-    return CYAES_OK;
-}
-
-// Appends n requests to the calling thread's shard (one lock) and wakes the
-// builder when the queue was empty or the batch is now full.
-void cyaes_batcher::enqueue(Req* rs, size_t n, uint64_t nbytes) {
-    if (n == 0) return;
-    const auto t = Clock::now();
-    const int s = my_shard();
-    Shard& sh = shards[s];
-    {
-        std::lock_guard<std::mutex> lk(sh.mu);
-        for (size_t i = 0; i < n; i++) {
-            rs[i].t = t;
-            rs[i].seq = sh.enqueued + i + 1;
-            rs[i].shard = (uint8_t)s;
-            sh.q.push_back(std::move(rs[i]));
-        }
-        sh.bytes += nbytes;
-        sh.enqueued += n;
-    }
-    if (oldest_ns.load(std::memory_order_relaxed) == 0) {  // a plain load while a time is recorded
-        int64_t zero = 0;
-        oldest_ns.compare_exchange_strong(zero, std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                                    t.time_since_epoch()).count());
-    }
-    const int64_t before = queued_reqs.fetch_add((int64_t)n);
-    const int64_t b0 = queued_bytes.fetch_add((int64_t)nbytes), cap = cfg.max_batch_bytes;
-    if (before <= 0 || (b0 < cap && b0 + (int64_t)nbytes >= cap)) {
-        std::lock_guard<std::mutex> lk(mu);  // orders the wake-up after the builder's predicate check
-        cv_submit.notify_one();
-    }
+    return t;
 }
 
 extern "C" {
@@ -674,7 +680,9 @@ int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out) {
     if (c.max_delay_us == 0) c.max_delay_us = 100;
     if (c.inflight == 0) c.inflight = 3;
     if (c.workers == 0) c.workers = 4;
-    if (c.max_batch_bytes < 4096 || c.max_batch_bytes > (1u << 30) || c.inflight > 16 || c.workers > 64)
+    if (c.max_sessions == 0) c.max_sessions = 65536;
+    if (c.max_batch_bytes < 4096 || c.max_batch_bytes > (1u << 30) || c.inflight > 16 || c.workers > 64 ||
+        c.max_sessions > (1u << 22))
         return CYAES_EINVAL;
     cyaes_gpu* ctx = nullptr;
     int st = cyaes_gpu_create(c.device, &ctx);
@@ -682,29 +690,54 @@ int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out) {
     auto* b = new cyaes_batcher();
     b->cfg = c;
     b->ctx = ctx;
-    // A stage holds max_batch_bytes of data plus meta and schedules: cost() is at
-    // most (data + 16 + 352) per request, and data >= 16 unless the request is empty.
-    b->stage_cap = 2ull * c.max_batch_bytes + 64 * 1024;
+    // HBM stage: max_batch_bytes of data, plus 16 B of relay header room per
+    // request, rounded: the cut never lets a batch exceed it (a first request is
+    // always taken; submit caps a request at max_batch_bytes).
+    b->data_cap = (uint64_t)c.max_batch_bytes;
+    b->bounce_cap = (uint64_t)c.max_batch_bytes + 2 * 65536;
+    b->gather_waves = std::max(64, cyaes_gpu_num_cus(ctx) * 32);
+    b->key_cap = c.max_sessions;
     b->stages.resize(c.inflight);
     int dev_prev = 0;
     (void)hipGetDevice(&dev_prev);
     hipError_t e = hipSetDevice(c.device);
+    const uint64_t data_room = b->data_cap + 16ull * kMaxReqs + 4096;
     for (Stage& s : b->stages) {
-        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h), b->stage_cap, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d), b->stage_cap);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        const uint64_t meta = 2ull * kMaxReqs * sizeof(BatchDesc);
+        uint8_t* h = nullptr;
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&h), meta, hipHostMallocDefault);
+        if (e == hipSuccess) {
+            s.h_enc = reinterpret_cast<BatchDesc*>(h);
+            s.h_dec = s.h_enc + kMaxReqs;
+            e = hipHostMalloc(reinterpret_cast<void**>(&s.h_bounce), b->bounce_cap, hipHostMallocMapped);
+        }
+        if (e == hipSuccess) {
+            void* dp = nullptr;
+            e = hipHostGetDevicePointer(&dp, s.h_bounce, 0);
+            s.bounce_dev = (uint64_t)(uintptr_t)dp;
+        }
+        const uint64_t lists = (uint64_t)kMaxReqs * (sizeof(BatchDesc) + 8 + 4 + 4);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_mem), lists + data_room);
+        if (e == hipSuccess) {
+            s.d_desc = reinterpret_cast<BatchDesc*>(s.d_mem);
+            s.d_offs = reinterpret_cast<uint64_t*>(s.d_desc + kMaxReqs);
+            s.d_nb = reinterpret_cast<uint32_t*>(s.d_offs + kMaxReqs);
+            s.d_kid = s.d_nb + kMaxReqs;
+            s.d_data = reinterpret_cast<uint8_t*>(s.d_kid + kMaxReqs);
+            e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
-        s.cap = b->stage_cap;
+        s.cbs.reserve(kMaxReqs);
         b->free_stages.push_back(&s);
     }
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&b->d_keys), (uint64_t)b->key_cap * kSchedBytes);
     (void)hipSetDevice(dev_prev);
     if (e != hipSuccess) {
         b->builder_done = true;
         cyaes_batcher_destroy(b);
         return map_err(e);
     }
-    b->gather_pool.reset(new Pool((int)c.workers - 1));  // + the builder thread itself
-    b->scatter_pool.reset(new Pool((int)c.workers - 1)); // + the completion thread itself
+    b->workers.reset(new Pool((int)c.workers - 1));  // + the builder / completion thread itself
     b->builder = std::thread([b] {
         (void)hipSetDevice(b->cfg.device);
         b->build_loop();
@@ -730,20 +763,28 @@ void cyaes_batcher_destroy(cyaes_batcher* b) {
         const Phases &B = b->pb, &C = b->pc;
         const double nb = (double)C.batches, us = 1e-3;
         fprintf(stderr,
-                "[cyaes_batcher] %lld batches, %.0f reqs/batch; per batch (us): builder wait %.0f take %.0f form %.0f "
-                "layout %.0f gather %.0f submit %.0f | completer sync %.0f scatter %.0f callbacks %.0f\n",
-                (long long)C.batches, C.reqs / nb, B.wait * us / nb, B.take * us / nb, B.form * us / nb,
-                B.layout * us / nb, B.gather * us / nb, B.submit * us / nb, C.sync * us / nb, C.scatter * us / nb,
-                C.callbacks * us / nb);
+                "[cyaes_batcher] %lld batches, %.0f reqs/batch; per batch (us): builder wait %.0f take %.0f layout "
+                "%.0f copy-in %.0f submit %.0f | completer sync %.0f copy-out %.0f callbacks %.0f\n",
+                (long long)C.batches, C.reqs / nb, B.wait * us / nb, B.take * us / nb, B.layout * us / nb,
+                B.copy_in * us / nb, B.submit * us / nb, C.sync * us / nb, C.copy_out * us / nb, C.callbacks * us / nb);
     }
+    b->workers.reset();
+    int dev_prev = 0;
+    (void)hipGetDevice(&dev_prev);
+    (void)hipSetDevice(b->cfg.device);
     for (Stage& s : b->stages) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.stream) (void)hipStreamDestroy(s.stream);
-        if (s.d) (void)hipFree(s.d);
-        if (s.h) (void)hipHostFree(s.h);
+        if (s.d_mem) (void)hipFree(s.d_mem);
+        if (s.h_enc) (void)hipHostFree(s.h_enc);
+        if (s.h_bounce) (void)hipHostFree(s.h_bounce);
     }
-    cyaes_gpu_destroy(b->ctx);
+    if (b->d_keys) (void)hipFree(b->d_keys);
+    for (PoolEnt& p : b->pools)
+        if (p.live && p.owned) (void)hipHostUnregister(p.pinned);
+    (void)hipSetDevice(dev_prev);
+    (void)cyaes_gpu_destroy(b->ctx);
     delete b;
 }
 
@@ -751,13 +792,48 @@ int cyaes_batcher_session_open(cyaes_batcher* b, const uint8_t key[16], uint32_t
     if (!b || !key || !slot) return CYAES_EINVAL;
     cyaes_key k;
     cyaes::expand_key(key, &k);
-    auto s = std::make_shared<Sched>();
-    cyaes::to_device_schedule(k, s->data());
+    uint32_t sched[cyaes::kSchedWords];
+    cyaes::to_device_schedule(k, sched);
     std::lock_guard<std::mutex> lk(b->smu);
+    // Rows retired by closes whose earlier requests have all completed are free again.
+    if (!b->retired.empty()) {
+        std::array<uint64_t, kShards> done;
+        {
+            std::lock_guard<std::mutex> l2(b->mu);
+            done = b->done_seq;
+        }
+        auto it = std::remove_if(b->retired.begin(), b->retired.end(), [&](const cyaes_batcher::Retired& r) {
+            for (int i = 0; i < kShards; i++)
+                if (done[i] < r.stamp[i]) return false;
+            b->free_rows.push_back(r.row);
+            return true;
+        });
+        b->retired.erase(it, b->retired.end());
+    }
+    uint32_t row;
+    if (!b->free_rows.empty()) {
+        row = b->free_rows.back();
+        b->free_rows.pop_back();
+    } else if (b->next_row < b->key_cap) {
+        row = b->next_row++;
+    } else {
+        return CYAES_ERANGE;  // max_sessions rows in use (or still referenced by queued requests)
+    }
+    int dev_prev = 0;
+    (void)hipGetDevice(&dev_prev);
+    (void)hipSetDevice(b->cfg.device);
+    // Synchronous: every batch built after this returns sees the row.
+    const hipError_t e = hipMemcpy(reinterpret_cast<uint8_t*>(b->d_keys) + (uint64_t)row * kSchedBytes, sched,
+                                   kSchedBytes, hipMemcpyHostToDevice);
+    (void)hipSetDevice(dev_prev);
+    if (e != hipSuccess) {
+        b->free_rows.push_back(row);
+        return map_err(e);
+    }
     size_t i = 0;
-    while (i < b->sessions.size() && b->sessions[i]) i++;
-    if (i == b->sessions.size()) b->sessions.emplace_back();
-    b->sessions[i] = std::move(s);
+    while (i < b->slot_row.size() && b->slot_row[i] != kNoRow) i++;
+    if (i == b->slot_row.size()) b->slot_row.push_back(kNoRow);
+    b->slot_row[i] = row;
     b->sessions_version.fetch_add(1, std::memory_order_release);
     *slot = (uint32_t)i;
     return CYAES_OK;
@@ -766,91 +842,164 @@ int cyaes_batcher_session_open(cyaes_batcher* b, const uint8_t key[16], uint32_t
 int cyaes_batcher_session_close(cyaes_batcher* b, uint32_t slot) {
     if (!b) return CYAES_EINVAL;
     std::lock_guard<std::mutex> lk(b->smu);
-    if (slot >= b->sessions.size() || !b->sessions[slot]) return CYAES_ERANGE;
-    b->sessions[slot].reset();
+    if (slot >= b->slot_row.size() || b->slot_row[slot] == kNoRow) return CYAES_ERANGE;
+    const uint32_t row = b->slot_row[slot];
+    b->slot_row[slot] = kNoRow;
     b->sessions_version.fetch_add(1, std::memory_order_release);
+    // Stamp after the version bump: a request enqueued later sees the new version.
+    b->retired.push_back({row, enqueue_counts(b)});
     return CYAES_OK;
 }
 
-static int submit_one(cyaes_batcher* b, const cyaes_batch_req& q) {
-    if (b->stop.load()) return CYAES_EINVAL;
-    Req r;
-    const int st = b->make(q, b->snapshot(), &r);
-    if (st) return st;
-    b->enqueue(&r, 1, r.data_bytes());
+int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint32_t* pool) {
+    if (!b || !base || !bytes || !pool) return CYAES_EINVAL;
+    std::lock_guard<std::mutex> lk(b->pmu);
+    int slot = -1;
+    for (int i = 0; i < kMaxPools; i++) {
+        const PoolEnt& e = b->pools[i];
+        if (e.live && (uintptr_t)base < (uintptr_t)e.host + e.bytes && (uintptr_t)e.host < (uintptr_t)base + bytes)
+            return CYAES_EINVAL;  // overlaps a registered pool
+        if (!e.live && slot < 0) slot = i;
+    }
+    if (slot < 0) return CYAES_ENOMEM;
+    int dev_prev = 0;
+    (void)hipGetDevice(&dev_prev);
+    (void)hipSetDevice(b->cfg.device);
+    // Pin the whole pages the range covers (the caller's buffer need not be page aligned).
+    uint8_t* lo = reinterpret_cast<uint8_t*>((uintptr_t)base & ~(uintptr_t)4095);
+    const size_t span = (((uintptr_t)base + bytes + 4095) & ~(uintptr_t)4095) - (uintptr_t)lo;
+    bool owned = true;
+    hipError_t e = hipHostRegister(lo, span, hipHostRegisterMapped);
+    if (e == hipErrorHostMemoryAlreadyRegistered) {  // already pinned (hipHostMalloc'd): use it as it is
+        (void)hipGetLastError();
+        owned = false;
+        e = hipSuccess;
+    }
+    void* dev = nullptr;
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dev, base, 0);
+    if (e != hipSuccess && owned) (void)hipHostUnregister(lo);
+    (void)hipSetDevice(dev_prev);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return map_err(e);
+    }
+    b->pools[slot] = PoolEnt{static_cast<uint8_t*>(base), (uint64_t)(uintptr_t)dev, (uint64_t)bytes, true, owned, lo};
+    b->pools_version.fetch_add(1, std::memory_order_release);
+    *pool = (uint32_t)slot;
     return CYAES_OK;
 }
 
-int cyaes_batcher_submit(cyaes_batcher* b, int op, uint32_t slot, const uint8_t* in, uint8_t* out, size_t size,
-                         cyaes_done_fn done, void* user) {
-    if (!b || (op != CYAES_OP_ENCRYPT && op != CYAES_OP_DECRYPT) || size > 0xFFFFFFFFu) return CYAES_EINVAL;
-    return submit_one(b, cyaes_batch_req{op, slot, 0, in, out, (uint32_t)size, done, user});
-}
-
-int cyaes_batcher_submit_seal(cyaes_batcher* b, uint32_t slot, int32_t conn_id, const uint8_t* payload,
-                              uint32_t size, uint8_t* packet_out, cyaes_done_fn done, void* user) {
-    if (!b) return CYAES_EINVAL;
-    return submit_one(b, cyaes_batch_req{CYAES_OP_RELAY_SEAL, slot, conn_id, payload, packet_out, size, done, user});
-}
-
-int cyaes_batcher_submit_open(cyaes_batcher* b, uint32_t slot, uint8_t* packet, uint32_t packet_bytes,
-                              cyaes_done_fn done, void* user) {
-    if (!b) return CYAES_EINVAL;
-    return submit_one(b, cyaes_batch_req{CYAES_OP_RELAY_OPEN, slot, 0, packet, packet, packet_bytes, done, user});
+int cyaes_batcher_unregister_pool(cyaes_batcher* b, uint32_t pool) {
+    if (!b || pool >= (uint32_t)kMaxPools) return CYAES_EINVAL;
+    PoolEnt ent;
+    {
+        std::lock_guard<std::mutex> lk(b->pmu);
+        if (!b->pools[pool].live) return CYAES_EINVAL;
+        ent = b->pools[pool];
+        b->pools[pool].live = false;
+        b->pools_version.fetch_add(1, std::memory_order_release);
+    }
+    // Requests enqueued before the removal may still read or write the pool.
+    (void)b->wait_enqueued(enqueue_counts(b));
+    if (ent.owned) {
+        int dev_prev = 0;
+        (void)hipGetDevice(&dev_prev);
+        (void)hipSetDevice(b->cfg.device);
+        const hipError_t e = hipHostUnregister(ent.pinned);
+        (void)hipSetDevice(dev_prev);
+        if (e != hipSuccess) return map_err(e);
+    }
+    return CYAES_OK;
 }
 
 int cyaes_batcher_submit_many(cyaes_batcher* b, const cyaes_batch_req* reqs, uint32_t n, int* status) {
     if (!b || (n && !reqs)) return CYAES_EINVAL;
     if (b->stop.load()) return CYAES_EINVAL;
-    std::vector<Req> rs(n);
-    size_t k = 0;
-    uint64_t nbytes = 0;
-    int first = CYAES_OK;
-    const SessionSnap& ss = b->snapshot();
-    for (uint32_t i = 0; i < n; i++) {
-        const int st = b->make(reqs[i], ss, &rs[k]);
-        if (status) status[i] = st;
-        if (st) {
-            if (first == CYAES_OK) first = st;
-            continue;
+    return b->enqueue([&](const Snap& ss, std::vector<Pend>& ps, uint64_t& nbytes) {
+        int first = CYAES_OK;
+        ps.resize(n);
+        size_t k = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const int st = b->make(reqs[i], ss, &ps[k]);
+            if (status) status[i] = st;
+            if (st) {
+                if (first == CYAES_OK) first = st;
+                continue;
+            }
+            nbytes += stage_bytes(ps[k].d);
+            k++;
         }
-        nbytes += rs[k].data_bytes();
-        k++;
-    }
-    b->enqueue(rs.data(), k, nbytes);
-    return first;
+        ps.resize(k);
+        return first;
+    });
+}
+
+int cyaes_batcher_submit_pooled(cyaes_batcher* b, const cyaes_pool_req* reqs, uint32_t n, int* status) {
+    if (!b || (n && !reqs)) return CYAES_EINVAL;
+    if (b->stop.load()) return CYAES_EINVAL;
+    return b->enqueue([&](const Snap& ss, std::vector<Pend>& ps, uint64_t& nbytes) {
+        int first = CYAES_OK;
+        ps.resize(n);
+        size_t k = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const int st = b->make_pooled(reqs[i], ss, &ps[k]);
+            if (status) status[i] = st;
+            if (st) {
+                if (first == CYAES_OK) first = st;
+                continue;
+            }
+            nbytes += stage_bytes(ps[k].d);
+            k++;
+        }
+        ps.resize(k);
+        return first;
+    });
+}
+
+int cyaes_batcher_submit(cyaes_batcher* b, int op, uint32_t slot, const uint8_t* in, uint8_t* out, size_t size,
+                         cyaes_done_fn done, void* user) {
+    if (!b || (op != CYAES_OP_ENCRYPT && op != CYAES_OP_DECRYPT) || size > 0xFFFFFFFFu) return CYAES_EINVAL;
+    const cyaes_batch_req q{op, slot, 0, in, out, (uint32_t)size, done, user};
+    int st = CYAES_OK;
+    const int rc = cyaes_batcher_submit_many(b, &q, 1, &st);
+    return rc ? rc : st;
+}
+
+int cyaes_batcher_submit_seal(cyaes_batcher* b, uint32_t slot, int32_t conn_id, const uint8_t* payload,
+                              uint32_t size, uint8_t* packet_out, cyaes_done_fn done, void* user) {
+    if (!b) return CYAES_EINVAL;
+    const cyaes_batch_req q{CYAES_OP_RELAY_SEAL, slot, conn_id, payload, packet_out, size, done, user};
+    int st = CYAES_OK;
+    const int rc = cyaes_batcher_submit_many(b, &q, 1, &st);
+    return rc ? rc : st;
+}
+
+int cyaes_batcher_submit_open(cyaes_batcher* b, uint32_t slot, uint8_t* packet, uint32_t packet_bytes,
+                              cyaes_done_fn done, void* user) {
+    if (!b) return CYAES_EINVAL;
+    const cyaes_batch_req q{CYAES_OP_RELAY_OPEN, slot, 0, packet, packet, packet_bytes, done, user};
+    int st = CYAES_OK;
+    const int rc = cyaes_batcher_submit_many(b, &q, 1, &st);
+    return rc ? rc : st;
 }
 
 int cyaes_batcher_flush(cyaes_batcher* b) {
     if (!b) return CYAES_EINVAL;
-    std::array<uint64_t, kShards> target;  // every shard's queue length at the call
-    for (int i = 0; i < kShards; i++) {
-        std::lock_guard<std::mutex> sl(b->shards[i].mu);
-        target[i] = b->shards[i].enqueued;
-    }
-    std::unique_lock<std::mutex> lk(b->mu);
-    b->flushers.fetch_add(1);
-    b->cv_submit.notify_all();
-    b->cv_flush.wait(lk, [&] {
-        for (int i = 0; i < kShards; i++)
-            if (b->done_seq[i] < target[i]) return false;
-        return true;
-    });
-    b->flushers.fetch_sub(1);
-    const int err = b->first_error;
-    b->first_error = CYAES_OK;
-    return err;
+    return b->wait_enqueued(enqueue_counts(b));
 }
 
 int cyaes_batcher_stats(cyaes_batcher* b, uint64_t out[6]) {
     if (!b || !out) return CYAES_EINVAL;
-    std::lock_guard<std::mutex> lk(b->mu);  // completed cannot grow while held: pending >= 0
+    const std::array<uint64_t, kShards> enq = enqueue_counts(b);
+    std::lock_guard<std::mutex> lk(b->mu);
+    uint64_t total = 0;
+    for (uint64_t v : enq) total += v;
     out[0] = b->completed;
     out[1] = b->batches;
     out[2] = b->bytes;
     out[3] = b->max_batch;
     out[4] = b->errors;
-    out[5] = b->enqueued_total() - b->completed;
+    out[5] = total >= b->completed ? total - b->completed : 0;
     return CYAES_OK;
 }
 

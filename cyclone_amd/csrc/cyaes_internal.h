@@ -124,6 +124,27 @@ hipError_t launch_fill_synthetic(uint8_t* buf, uint64_t p0, uint64_t npayloads, 
                                  uint64_t seed, hipStream_t stream);
 hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long* out2, hipStream_t stream);
 
+// Batching adapter request descriptor (cyaes_batcher.cpp builds them in pinned
+// memory, cyaes_batch_kernels.hip reads them).  src / dst are DEVICE
+// addresses: a registered host packet pool (mapped) or the batcher's bounce
+// buffer.  Op codes = CYAES_OP_* (cyaes_batch.h).
+constexpr uint32_t kOpEncrypt = 0, kOpDecrypt = 1, kOpRelaySeal = 2, kOpRelayOpen = 3;
+struct BatchDesc {
+    uint64_t src;    // ENCRYPT/DECRYPT: input; SEAL: chunk; OPEN: packet
+    uint64_t dst;    // ENCRYPT/DECRYPT: output; SEAL: packet out; OPEN: the packet (in place)
+    uint32_t size;   // ENCRYPT/DECRYPT: bytes; SEAL: chunk bytes; OPEN: packet bytes
+    uint32_t crypt;  // bytes en/decrypted (SEAL: the chunk rounded up to 16)
+    uint32_t key;    // row of the batcher's device key table
+    int32_t conn;    // SEAL: RelayForwardMsg::id
+    uint32_t op;
+    uint32_t stage;  // byte offset of the request's data in the batch's HBM stage
+};
+static_assert(sizeof(BatchDesc) == 40, "BatchDesc layout");
+hipError_t launch_batch_gather(const BatchDesc* d_desc, uint32_t n, uint8_t* d_stage, uint64_t* d_offs,
+                               uint32_t* d_nbytes, uint32_t* d_kidx, int max_waves, hipStream_t stream);
+hipError_t launch_batch_scatter(const BatchDesc* d_desc, uint32_t n, const uint8_t* d_stage, int max_waves,
+                                hipStream_t stream);
+
 // Host runtime (cyaes_runtime.cpp): ragged batch under an explicit device key
 // table of table_keys schedules (the batcher's per-batch session keys).
 // key_idx (device, nullable => key 0) indexes that table.

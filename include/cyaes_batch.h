@@ -6,16 +6,27 @@
  * 365; relay_server.cpp:329, 453-481).  A single packet is one CBC chain of
  * at most 4,080 blocks, so on a GPU it is all latency.  This adapter takes
  * those calls from any number of threads, coalesces whatever arrives within
- * a short window into one pinned staging buffer (gather), runs one ragged
- * batch on the MI355X, copies the results back to the callers' buffers
- * (scatter) and invokes each request's completion callback -- where a relay
- * would then post TcpConnection::send to its looper.
+ * a short window into one GPU batch and invokes each request's completion
+ * callback -- where a relay would then post TcpConnection::send to its looper.
+ *
+ * Zero-copy packet pools: memory the caller registers once
+ * (cyaes_batcher_register_pool) is read and written by the GPU itself over
+ * PCIe: a batch's inputs are gathered from the pools into HBM by a kernel,
+ * SEAL packets are built there, the ragged AES kernels run, and a kernel
+ * scatters the outputs back into the pools.  The host copies no payload
+ * byte; its per-request work is a 40-byte descriptor.  A request whose
+ * buffers lie in registered pools takes this path automatically (pointer
+ * submits) or explicitly (cyaes_batcher_submit_pooled, pool offsets).
+ * Buffers outside every pool are copied through the batcher's pinned bounce
+ * memory instead (same results, host copies in and out).
  *
  * Sessions (row 3): every request names a session slot.  A slot holds the
  * key of one relay pipe direction (relay_server.cpp:218-240 creates the
  * Rijndael pair after the DH handshake; :370-375 deletes it on close).
- * Schedules are expanded once on open (host) and travel with each batch that
- * uses them, so opening/closing sessions never races in-flight batches.
+ * Its schedule is expanded once on open into a row of the batcher's device
+ * key table; a closed slot's row is reused only after every request
+ * submitted before the close has completed, so opening and closing sessions
+ * never races in-flight batches.
  *
  * Request semantics = Rijndael::encrypt / decrypt (cyr_rijndael.cpp:588-635)
  * with iv == nullptr, as every relay call site passes: one CBC chain from
@@ -26,10 +37,11 @@
  *   OPEN: decrypt a received RELAY_FORWARD packet's payload in place
  *         (relay_server.cpp:329).
  *
- * Pipelining: `inflight` staging buffers; while the GPU runs batch k the
- * builder thread gathers batch k+1 and the completion thread scatters k-1.
- * Callbacks run on the completion thread, in batch order; they must not
- * block on the batcher (flush/destroy) themselves.
+ * Pipelining: `inflight` stages; while the GPU runs batch k the builder lays
+ * out batch k+1 and the completion side runs k-1's callbacks.  Callbacks run
+ * on the completion thread and the worker threads, one submitting thread's
+ * requests in its submission order; they must not block on the batcher
+ * (flush/destroy/unregister) themselves.
  */
 #ifndef CYAES_BATCH_H
 #define CYAES_BATCH_H
@@ -55,8 +67,9 @@ typedef struct cyaes_batcher_config {
     int device;               /* HIP device                                          */
     uint32_t max_batch_bytes; /* staging bytes per batch (0 => 32 MiB); caps a request */
     uint32_t max_delay_us;    /* longest a request waits for company (0 => 100 us)     */
-    uint32_t inflight;        /* staging buffers / batches in flight (0 => 3)          */
-    uint32_t workers;         /* threads per gather / scatter of a batch (0 => 4)     */
+    uint32_t inflight;        /* stages / batches in flight (0 => 3)                   */
+    uint32_t workers;         /* completion-side threads: callbacks, bounce copies (0 => 4) */
+    uint32_t max_sessions;    /* device key-table rows (0 => 65536)                    */
 } cyaes_batcher_config;
 
 int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out);
@@ -101,6 +114,32 @@ typedef struct cyaes_batch_req {
     void* user;
 } cyaes_batch_req;
 int cyaes_batcher_submit_many(cyaes_batcher* b, const cyaes_batch_req* reqs, uint32_t n, int* status);
+
+/* Packet pools.  register: pins [base, base + bytes) for the device
+ * (hipHostRegister, mapped; memory already pinned by hipHostMalloc is used as
+ * it is) and returns a pool id; pools may not overlap (CYAES_EINVAL), at most
+ * 64 (CYAES_ENOMEM).  unregister: waits until every request submitted before
+ * the call has completed, then unpins.  Requests may not use the pool
+ * concurrently with its unregister. */
+int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint32_t* pool);
+int cyaes_batcher_unregister_pool(cyaes_batcher* b, uint32_t pool);
+
+/* Bulk submit by pool offsets (zero-copy).  Per request, as cyaes_batch_req
+ * with in = pool base + in_off and out = pool base + out_off (OPEN: the packet
+ * at in_off, decrypted in place; out_off ignored).  A request whose bytes do
+ * not lie inside the pool is CYAES_EINVAL. */
+typedef struct cyaes_pool_req {
+    int op;
+    uint32_t slot;
+    int32_t conn_id;
+    uint32_t pool;
+    uint64_t in_off;
+    uint64_t out_off;
+    uint32_t size;
+    cyaes_done_fn done;
+    void* user;
+} cyaes_pool_req;
+int cyaes_batcher_submit_pooled(cyaes_batcher* b, const cyaes_pool_req* reqs, uint32_t n, int* status);
 
 /* Blocks until every request submitted before the call has completed
  * (callbacks returned).  Returns the first error status seen since the

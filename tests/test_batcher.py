@@ -425,3 +425,150 @@ def test_device_relay_stream_config_b_default_kernels():
     assert ctx.check() == ca.CYAES_OK
     assert torch.equal(view[:, hdr:hdr + pb].reshape(-1), pt)
     ctx.close()
+
+
+# ---- zero-copy packet pools (round 3) ---------------------------------------
+def test_pooled_requests_zero_copy_match_oracle(batcher):
+    """Requests whose buffers lie in a registered pool are gathered from and
+    scattered to it by the GPU (cyaes_batch_kernels.hip): by pointer (found
+    in the pool automatically) and by pool offset (submit_pooled).  ENCRYPT,
+    DECRYPT, SEAL (relay_local.cpp:189-206) and OPEN (relay_server.cpp:329) at
+    16-, 4- and 1-byte aligned addresses, in place and not, against the AES
+    oracle and the relay restatement."""
+    import numpy as np
+    key = _keys(1, 21)[0]
+    slot = batcher.session_open(key)
+    aes = oracle.Rijndael(key)
+    rng = random.Random(21)
+    pool = np.zeros(8 << 20, dtype=np.uint8)
+    pid = batcher.register_pool(pool)
+    mv = memoryview(pool)
+    pos = [64]
+
+    def carve(n, align):
+        o = (pos[0] + 63) // 64 * 64 + align
+        pos[0] = o + n + 64
+        return o
+    checks, reqs = [], []
+    for i in range(160):
+        op = [ca.OP_ENCRYPT, ca.OP_DECRYPT, ca.OP_RELAY_SEAL, ca.OP_RELAY_OPEN][i % 4]
+        align = [0, 4, 12, 1][(i // 4) % 4]
+        if op in (ca.OP_ENCRYPT, ca.OP_DECRYPT):
+            n = 16 * rng.choice([0, 1, 5, 92, 300, 4080])
+            src = bytes(rng.getrandbits(8) for _ in range(n))
+            io = carve(n, align)
+            pool[io:io + n] = np.frombuffer(src, np.uint8)
+            inplace = i % 3 == 0
+            oo = io if inplace else carve(n, (align * 7) % 16)
+            want = (aes.decrypt if op == ca.OP_DECRYPT else aes.encrypt)(bytearray(src))
+            checks.append((oo, bytes(want)))
+            reqs.append((op, io, oo, n))
+        elif op == ca.OP_RELAY_SEAL:
+            n = rng.choice([0, 1, 17, 1472, 4000, 0xFF00])
+            chunk = bytes(rng.getrandbits(8) for _ in range(n))
+            io = carve(n, align)
+            pool[io:io + n] = np.frombuffer(chunk, np.uint8)
+            oo = carve(ca.relay_packet_bytes(n), (align + 4) % 16)
+            checks.append((oo, ro.seal_forward(key, 3000 + i, chunk)))
+            reqs.append((op, io, oo, n))
+        else:
+            n = rng.choice([16, 1472, 9000])
+            chunk = bytes(rng.getrandbits(8) for _ in range(n))
+            pkt = ro.seal_forward(key, 7, chunk)
+            io = carve(len(pkt), align)
+            pool[io:io + len(pkt)] = np.frombuffer(pkt, np.uint8)
+            checks.append((io, ro.open_forward(key, pkt)[2]))
+            reqs.append((op, io, None, len(pkt)))
+    status = []
+    half = len(reqs) // 2
+    for k, (op, io, oo, n) in enumerate(reqs[:half]):  # by pointer: found inside the pool
+        if op == ca.OP_RELAY_OPEN:
+            batcher.submit_open(slot, mv[io:io + n])
+        elif op == ca.OP_RELAY_SEAL:
+            batcher.submit_seal(slot, 3000 + k, mv[io:io + n], mv[oo:oo + ca.relay_packet_bytes(n)])
+        else:
+            batcher.submit(op, slot, mv[io:io + n], mv[oo:oo + n], n)
+    pooled = [(op, slot, pid, io, oo or 0, n, None, 3000 + half + k)
+              for k, (op, io, oo, n) in enumerate(reqs[half:])]
+    status = batcher.submit_pooled(pooled)
+    assert status == [0] * len(pooled)
+    assert batcher.flush() == ca.CYAES_OK
+    for k, (off, want) in enumerate(checks):
+        assert bytes(pool[off:off + len(want)]) == want, k
+    # a pooled request that runs past its pool's end is rejected
+    bad = batcher.submit_pooled([(ca.OP_ENCRYPT, slot, pid, pool.size - 16, 0, 32, None, 0)])
+    assert bad == [ca.CYAES_EINVAL]
+    batcher.unregister_pool(pid)
+    with pytest.raises(ca.CyaesError):
+        batcher.unregister_pool(pid)
+    batcher.session_close(slot)
+
+
+def test_pool_session_rows_survive_close_and_reopen(batcher):
+    """A closed slot's key row is not reused while requests submitted before
+    the close are still queued: pooled requests keep the key they were
+    submitted under across close/reopen churn (cyaes_batch.h, sessions)."""
+    import numpy as np
+    pool = np.zeros(4 << 20, dtype=np.uint8)
+    pid = batcher.register_pool(pool)
+    rng = random.Random(33)
+    want = []
+    off = 0
+    for rnd in range(40):
+        key = bytes(rng.getrandbits(8) for _ in range(16))
+        slot = batcher.session_open(key)
+        reqs = []
+        for _ in range(rng.randrange(1, 8)):
+            n = 16 * rng.choice([1, 92, 300])
+            data = bytes(rng.getrandbits(8) for _ in range(n))
+            pool[off:off + n] = np.frombuffer(data, np.uint8)
+            reqs.append((ca.OP_ENCRYPT, slot, pid, off, off + n, n, None, 0))
+            want.append((off + n, bytes(oracle.Rijndael(key).encrypt(bytearray(data)))))
+            off += 2 * n
+        assert batcher.submit_pooled(reqs) == [0] * len(reqs)
+        batcher.session_close(slot)
+    assert batcher.flush() == ca.CYAES_OK
+    for o, w in want:
+        assert bytes(pool[o:o + len(w)]) == w
+    batcher.unregister_pool(pid)
+
+
+def _bench_batcher_dump(tmp_path, op, extra=()):
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "build", "bench_batcher")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", root, "-s", "build/bench_batcher"], check=True)
+    dump = str(tmp_path / ("dump_%s.bin" % op))
+    cmd = [exe, "--op", op, "--threads", "3", "--window", "64", "--seconds", "0.3", "--dump", dump] + list(extra)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    import json
+    return json.loads(line), open(dump, "rb").read()
+
+
+@pytest.mark.parametrize("op,extra", [("seal", ()), ("open", ()), ("seal", ("--submit", "pooled")),
+                                      ("open", ("--pool", "0"))])
+def test_bench_batcher_output_matches_relay_oracle(tmp_path, op, extra):
+    """tools/bench_batcher's own packets (its --dump verification round: every
+    slot of every looper sealed or opened once through the zero-copy pool
+    path, or the bounce path with --pool 0) against the relay restatement."""
+    res, blob = _bench_batcher_dump(tmp_path, op, extra)
+    assert res["errors"] == 0 and res["requests_per_s"] > 0
+    opc, size, in_n, out_n = struct.unpack_from("<4I", blob, 0)
+    pos, nchecked = 16, 0
+    while pos < len(blob):
+        key = blob[pos:pos + 16]
+        nslots = struct.unpack_from("<I", blob, pos + 16)[0]
+        pos += 20
+        for _ in range(nslots):
+            inp, out = blob[pos:pos + in_n], blob[pos + in_n:pos + in_n + out_n]
+            pos += in_n + out_n
+            if opc == ca.OP_RELAY_SEAL:
+                assert out == ro.seal_forward(key, 7, inp)
+            else:
+                assert out == ro.open_forward(key, inp)[2]
+            nchecked += 1
+    assert nchecked == 3 * 64

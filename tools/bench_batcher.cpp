@@ -9,9 +9,21 @@
 // for comparison the synchronous drop-in path (cyaes_cbc_encrypt, one packet
 // per call, as the reference calls Rijndael::encrypt).
 //
+// Packet memory: by default every looper's slots are carved from one host
+// region registered as a zero-copy pool (cyaes_batcher_register_pool), so the
+// GPU gathers and scatters the packets itself; --pool 0 uses plain heap
+// buffers (the bounce path: host copies in and out).  --submit pooled sends
+// pool offsets (cyaes_batcher_submit_pooled) instead of pointers.  OPEN
+// re-opens each slot's packet in place every round (the work is the same
+// whatever the payload bytes are; --reopen-copy 1 restores the sealed packet
+// with a host memcpy first, load-generator work).  --dump FILE writes every
+// slot's input and output after a verification round (tests/ checks them
+// against the relay restatement).
+//
 // usage: bench_batcher [--op seal|open|enc|dec] [--size B] [--threads T]
 //                      [--window W] [--seconds S] [--batch-mb M] [--delay-us D]
-//                      [--workers K] [--inflight I] [--bulk 0|1]
+//                      [--workers K] [--inflight I] [--bulk 0|1] [--pool 0|1]
+//                      [--submit ptr|pooled] [--reopen-copy 0|1] [--dump FILE]
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -31,7 +43,9 @@
 using Clock = std::chrono::steady_clock;
 
 struct Slot {
-    std::vector<uint8_t> in, out;
+    uint8_t *in = nullptr, *out = nullptr;  // in the looper's memory (a registered pool by default)
+    uint32_t in_n = 0, out_n = 0;
+    uint64_t in_off = 0, out_off = 0;       // offsets in the pool
     Clock::time_point t0;
     struct Looper* owner = nullptr;
 };
@@ -41,6 +55,9 @@ struct Looper {
     uint32_t session = 0;
     int op = CYAES_OP_RELAY_SEAL;
     uint32_t size = 1472;
+    uint8_t* mem = nullptr;  // the slots' buffers
+    uint32_t pool = ~0u;     // registered pool id (~0u: not registered)
+    bool pooled_submit = false, reopen_copy = false;
     std::vector<Slot> slots;
     std::mutex mu;
     std::vector<Slot*> ready;  // completed, to resubmit
@@ -64,12 +81,12 @@ static int submit(Looper* L, Slot* s) {
     s->t0 = Clock::now();
     switch (L->op) {
         case CYAES_OP_RELAY_SEAL:
-            return cyaes_batcher_submit_seal(L->b, L->session, 7, s->in.data(), L->size, s->out.data(), on_done, s);
-        case CYAES_OP_RELAY_OPEN:  // re-open the same sealed packet: the work is the same every time
-            memcpy(s->out.data(), s->in.data(), s->in.size());
-            return cyaes_batcher_submit_open(L->b, L->session, s->out.data(), (uint32_t)s->out.size(), on_done, s);
+            return cyaes_batcher_submit_seal(L->b, L->session, 7, s->in, L->size, s->out, on_done, s);
+        case CYAES_OP_RELAY_OPEN:  // re-open the slot's packet in place: the work is the same every time
+            if (L->reopen_copy) memcpy(s->out, s->in, s->in_n);
+            return cyaes_batcher_submit_open(L->b, L->session, s->out, s->out_n, on_done, s);
         default:
-            return cyaes_batcher_submit(L->b, L->op, L->session, s->in.data(), s->out.data(), L->size, on_done, s);
+            return cyaes_batcher_submit(L->b, L->op, L->session, s->in, s->out, L->size, on_done, s);
     }
 }
 
@@ -77,12 +94,25 @@ static cyaes_batch_req make_req(Looper* L, Slot* s) {
     s->t0 = Clock::now();
     switch (L->op) {
         case CYAES_OP_RELAY_SEAL:
-            return {CYAES_OP_RELAY_SEAL, L->session, 7, s->in.data(), s->out.data(), L->size, on_done, s};
+            return {CYAES_OP_RELAY_SEAL, L->session, 7, s->in, s->out, L->size, on_done, s};
         case CYAES_OP_RELAY_OPEN:
-            memcpy(s->out.data(), s->in.data(), s->in.size());
-            return {CYAES_OP_RELAY_OPEN, L->session, 0, nullptr, s->out.data(), (uint32_t)s->out.size(), on_done, s};
+            if (L->reopen_copy) memcpy(s->out, s->in, s->in_n);
+            return {CYAES_OP_RELAY_OPEN, L->session, 0, nullptr, s->out, s->out_n, on_done, s};
         default:
-            return {L->op, L->session, 0, s->in.data(), s->out.data(), L->size, on_done, s};
+            return {L->op, L->session, 0, s->in, s->out, L->size, on_done, s};
+    }
+}
+
+static cyaes_pool_req make_pool_req(Looper* L, Slot* s) {
+    s->t0 = Clock::now();
+    switch (L->op) {
+        case CYAES_OP_RELAY_SEAL:
+            return {CYAES_OP_RELAY_SEAL, L->session, 7, L->pool, s->in_off, s->out_off, L->size, on_done, s};
+        case CYAES_OP_RELAY_OPEN:
+            if (L->reopen_copy) memcpy(s->out, s->in, s->in_n);
+            return {CYAES_OP_RELAY_OPEN, L->session, 0, L->pool, s->out_off, 0, s->out_n, on_done, s};
+        default:
+            return {L->op, L->session, 0, L->pool, s->in_off, s->out_off, L->size, on_done, s};
     }
 }
 
@@ -96,6 +126,8 @@ static double pct(std::vector<double>& v, double p) {
 int main(int argc, char** argv) {
     std::string op = "seal";
     uint32_t size = 1472, threads = 8, window = 512, batch_mb = 32, delay_us = 100, workers = 0, inflight = 3, bulk = 1;
+    uint32_t use_pool = 1, reopen_copy = 0;
+    std::string submit_kind = "ptr", dump;
     double seconds = 5;
     for (int i = 1; i + 1 < argc; i += 2) {
         std::string a = argv[i];
@@ -109,13 +141,22 @@ int main(int argc, char** argv) {
         else if (a == "--workers") workers = atoi(argv[i + 1]);
         else if (a == "--inflight") inflight = atoi(argv[i + 1]);
         else if (a == "--bulk") bulk = atoi(argv[i + 1]);
+        else if (a == "--pool") use_pool = atoi(argv[i + 1]);
+        else if (a == "--submit") submit_kind = argv[i + 1];
+        else if (a == "--reopen-copy") reopen_copy = atoi(argv[i + 1]);
+        else if (a == "--dump") dump = argv[i + 1];
+    }
+    const bool pooled_submit = submit_kind == "pooled";
+    if (pooled_submit && !use_pool) {
+        fprintf(stderr, "--submit pooled needs --pool 1\n");
+        return 1;
     }
     const int opc = op == "seal" ? CYAES_OP_RELAY_SEAL : op == "open" ? CYAES_OP_RELAY_OPEN
                     : op == "dec" ? CYAES_OP_DECRYPT : CYAES_OP_ENCRYPT;
     if ((opc == CYAES_OP_ENCRYPT || opc == CYAES_OP_DECRYPT) && size % 16) size = cyaes_relay_round16(size);
     if (opc >= CYAES_OP_RELAY_SEAL && size > CYAES_RELAY_MAX_CHUNK) size = CYAES_RELAY_MAX_CHUNK;
 
-    cyaes_batcher_config cfg = {0, batch_mb << 20, delay_us, inflight, workers};
+    cyaes_batcher_config cfg = {0, batch_mb << 20, delay_us, inflight, workers, 0};
     cyaes_batcher* b = nullptr;
     int st = cyaes_batcher_create(&cfg, &b);
     if (st) {
@@ -123,24 +164,68 @@ int main(int argc, char** argv) {
         return 1;
     }
     std::vector<Looper> loopers(threads);
+    const uint32_t pkt = cyaes_relay_packet_bytes(size);
+    const uint32_t in_n = opc == CYAES_OP_RELAY_OPEN ? pkt : size;
+    const uint32_t out_n = opc >= CYAES_OP_RELAY_SEAL ? pkt : size;
+    const uint64_t in_stride = (in_n + 63) & ~63u, out_stride = (out_n + 63) & ~63u;
     for (uint32_t t = 0; t < threads; t++) {
         Looper& L = loopers[t];
         L.b = b;
         L.op = opc;
         L.size = size;
+        L.pooled_submit = pooled_submit;
+        L.reopen_copy = reopen_copy != 0;
         uint8_t key[16];
         for (int i = 0; i < 16; i++) key[i] = (uint8_t)(t * 16 + i);
         cyaes_batcher_session_open(b, key, &L.session);
+        const uint64_t bytes = (uint64_t)window * (in_stride + out_stride);
+        L.mem = static_cast<uint8_t*>(aligned_alloc(4096, (bytes + 4095) & ~4095ull));
+        memset(L.mem, 0, bytes);
+        if (use_pool && (st = cyaes_batcher_register_pool(b, L.mem, bytes, &L.pool)) != CYAES_OK) {
+            fprintf(stderr, "cyaes_batcher_register_pool: %s\n", cyaes_strerror(st));
+            return 1;
+        }
         L.slots.resize(window);
         for (uint32_t w = 0; w < window; w++) {
             Slot& s = L.slots[w];
             s.owner = &L;
-            const uint32_t pkt = cyaes_relay_packet_bytes(size);
-            s.in.resize(opc == CYAES_OP_RELAY_OPEN ? pkt : size);
-            s.out.resize(opc >= CYAES_OP_RELAY_SEAL ? pkt : size);
-            for (size_t i = 0; i < s.in.size(); i++) s.in[i] = (uint8_t)(i * 131 + w);
-            if (opc == CYAES_OP_RELAY_OPEN) cyaes_relay_build_forward(s.in.data(), 7, s.in.data() + 12, size);
+            s.in_off = (uint64_t)w * in_stride;
+            s.out_off = (uint64_t)window * in_stride + (uint64_t)w * out_stride;
+            s.in = L.mem + s.in_off;
+            s.out = L.mem + s.out_off;
+            s.in_n = in_n;
+            s.out_n = out_n;
+            for (size_t i = 0; i < in_n; i++) s.in[i] = (uint8_t)(i * 131 + w + 7 * t);
+            if (opc == CYAES_OP_RELAY_OPEN) {
+                cyaes_relay_build_forward(s.in, 7, s.in + 12, size);
+                memcpy(s.out, s.in, in_n);
+            }
         }
+    }
+    // Verification round (--dump): every slot once, then inputs and outputs to FILE.
+    if (!dump.empty()) {
+        for (auto& L : loopers)
+            for (auto& s : L.slots) submit(&L, &s);
+        cyaes_batcher_flush(b);
+        FILE* f = fopen(dump.c_str(), "wb");
+        if (!f) return 1;
+        const uint32_t hdr[4] = {(uint32_t)opc, size, in_n, out_n};
+        fwrite(hdr, sizeof(hdr), 1, f);
+        for (auto& L : loopers) {
+            uint8_t key[16];
+            for (int i = 0; i < 16; i++) key[i] = (uint8_t)((&L - loopers.data()) * 16 + i);
+            const uint32_t nslots = (uint32_t)L.slots.size();
+            fwrite(key, 16, 1, f);
+            fwrite(&nslots, 4, 1, f);
+            for (auto& s : L.slots) {
+                fwrite(s.in, 1, in_n, f);
+                fwrite(s.out, 1, out_n, f);
+            }
+        }
+        fclose(f);
+        if (opc == CYAES_OP_RELAY_OPEN)  // restore the sealed packets for the timed rounds
+            for (auto& L : loopers)
+                for (auto& s : L.slots) memcpy(s.out, s.in, in_n);
     }
     // Warm-up: one window per looper.
     for (auto& L : loopers)
@@ -162,6 +247,7 @@ int main(int argc, char** argv) {
             for (auto& s : L.slots) submit(&L, &s);
             std::vector<Slot*> again;
             std::vector<cyaes_batch_req> reqs;
+            std::vector<cyaes_pool_req> preqs;
             while (!stop.load(std::memory_order_relaxed)) {
                 {
                     std::lock_guard<std::mutex> lk(L.mu);
@@ -171,7 +257,11 @@ int main(int argc, char** argv) {
                     std::this_thread::sleep_for(std::chrono::microseconds(20));
                     continue;
                 }
-                if (bulk) {  // one cyaes_batcher_submit_many per poll, as a relay looper would
+                if (bulk && L.pooled_submit) {  // one cyaes_batcher_submit_pooled per poll, by pool offsets
+                    preqs.clear();
+                    for (Slot* s : again) preqs.push_back(make_pool_req(&L, s));
+                    cyaes_batcher_submit_pooled(L.b, preqs.data(), (uint32_t)preqs.size(), nullptr);
+                } else if (bulk) {  // one cyaes_batcher_submit_many per poll, as a relay looper would
                     reqs.clear();
                     for (Slot* s : again) reqs.push_back(make_req(&L, s));
                     cyaes_batcher_submit_many(L.b, reqs.data(), (uint32_t)reqs.size(), nullptr);
@@ -204,6 +294,7 @@ int main(int argc, char** argv) {
     const double batches = (double)(st1[1] - st0[1]);
     const double p50 = pct(lat, 0.5), p99 = pct(lat, 0.99);
     cyaes_batcher_destroy(b);
+    for (auto& L : loopers) free(L.mem);
 
     // Synchronous drop-in for comparison: one packet per call (relay_local.cpp:206 shape).
     cyaes_key k;
@@ -221,11 +312,12 @@ int main(int argc, char** argv) {
 
     printf("{\"metric\": \"batcher %s requests/s host-to-host\", \"op\": \"%s\", \"size\": %u, \"threads\": %u, "
            "\"window\": %u, \"batch_mb\": %u, \"delay_us\": %u, \"workers\": %u, \"inflight\": %u, \"bulk\": %u, "
-           "\"seconds\": %.2f, \"requests\": %llu, "
+           "\"pool\": %u, \"submit\": \"%s\", \"seconds\": %.2f, \"requests\": %llu, "
            "\"requests_per_s\": %.0f, \"payload_gibs\": %.3f, \"mean_batch\": %.1f, \"lat_p50_us\": %.0f, "
            "\"lat_p99_us\": %.0f, \"errors\": %d, \"sync_dropin_calls_per_s\": %.0f, "
            "\"sync_dropin_gibs\": %.4f}\n",
-           op.c_str(), op.c_str(), size, threads, window, batch_mb, delay_us, workers, inflight, bulk, el, (unsigned long long)counted,
+           op.c_str(), op.c_str(), size, threads, window, batch_mb, delay_us, workers, inflight, bulk, use_pool,
+           submit_kind.c_str(), el, (unsigned long long)counted,
            counted / el, counted * payload / el / (1u << 30), batches > 0 ? (st1[0] - st0[0]) / batches : 0.0, p50,
            p99, err, calls / sync_s, calls * (double)buf.size() / sync_s / (1u << 30));
     return err ? 2 : 0;

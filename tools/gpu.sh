@@ -10,7 +10,8 @@
 #   bench      python bench.py (default: config E headline + packet configs + relay stream)
 #   quickbench bench.py --steps 3 --warmup 1 (no CPU baseline)
 #   profile    rocprofv3 --kernel-trace --stats of a short bench, then FETCH_SIZE / WRITE_SIZE PMC passes
-#   batcher    build/bench_batcher SEAL / OPEN loads (host to host)
+#   batchertest  tests/test_batcher.py only
+#   batcher    build/bench_batcher SEAL / OPEN loads (host to host), zero-copy and bounce ($BB_ARGS appended)
 #   hostlink   build/hostlink: kernel-driven packet gather/scatter over PCIe vs DMA
 #   ab:A:B[:ARGS]  tools/ab.py on variant libraries build/variants/{A,B}.so, both orders
 #                  (ARGS: extra ab.py arguments, commas for spaces)
@@ -50,7 +51,13 @@ for step in "$@"; do
           -- python3 "$R/bench.py" --config C --steps 2 --warmup 0 --no-cpu --no-verify --no-clock \
              --packet-configs none --relay-stream 0) || exit $?
       done ;;
-    batcher) run bench_batcher 300 build/bench_batcher ;;
+    batchertest) run pytest_batcher 300 python -u -m pytest tests/test_batcher.py -m gpu -x -v --timeout 150 --timeout-method thread ;;
+    batcher)  # SEAL / OPEN host to host: zero-copy pools (pointer and offset submits), then the bounce path
+      : > "$O/bench_batcher.jsonl"
+      for cfg in "seal --pool 1" "seal --submit pooled" "open --pool 1" "open --submit pooled" "seal --pool 0" "open --pool 0"; do
+        run bench_batcher_one 120 build/bench_batcher --op $cfg --threads 8 --window 8192 --seconds 4 ${BB_ARGS:-}
+        grep '^{' "$O/bench_batcher_one.txt" >> "$O/bench_batcher.jsonl"
+      done ;;
     hostlink) run hostlink 240 build/hostlink ;;
     ab:*)
       IFS=: read -r _ A B ARGS <<< "$step"
