@@ -281,7 +281,9 @@ struct cyaes_batcher {
     std::atomic<uint64_t> pools_version{1};
 
     const uint64_t id = g_batcher_ids.fetch_add(1);
-    std::unique_ptr<Pool> workers;  // bounce copies, callbacks
+    // One job at a time per pool: the builder's (bounce input copies) and the
+    // completion side's (bounce output copies, callbacks) run concurrently.
+    std::unique_ptr<Pool> in_pool, workers;
     std::thread builder, completer;
     Phases pb, pc;
 
@@ -438,6 +440,9 @@ void cyaes_batcher::build_loop() {
     std::array<std::vector<Pend>, kShards> pend, spare;  // builder-private: taken, not yet batched
     std::array<size_t, kShards> ppos{};
     std::array<uint64_t, kShards> batched{};  // per shard: requests put into batches so far
+    // (to, from, bytes) of the bounced requests' inputs; the workers run the
+    // copies, so this is a plain local (a thread_local would be theirs, empty).
+    std::vector<std::array<const uint8_t*, 3>> copies;
     int rr = 0;
     for (;;) {
         Stage* st = nullptr;
@@ -496,7 +501,6 @@ void cyaes_batcher::build_loop() {
         st->bouts.clear();
         uint64_t data = 0, bounce = 0;
         bool full = false;
-        thread_local std::vector<std::array<const uint8_t*, 3>> copies;  // (to, from, bytes) bounce inputs
         copies.clear();
         for (int k = 0; k < kShards && !full; k++) {
             const int s = (rr + k) % kShards;
@@ -554,7 +558,7 @@ void cyaes_batcher::build_loop() {
             free_stages.push_back(st);
             continue;
         }
-        workers->run(copies.size(), [&](size_t i) {
+        in_pool->run(copies.size(), [&](size_t i) {
             memcpy(const_cast<uint8_t*>(copies[i][0]), copies[i][1], (size_t)(uintptr_t)copies[i][2]);
         });
         const int64_t ts = now_ns();
@@ -737,7 +741,8 @@ int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out) {
         cyaes_batcher_destroy(b);
         return map_err(e);
     }
-    b->workers.reset(new Pool((int)c.workers - 1));  // + the builder / completion thread itself
+    b->in_pool.reset(new Pool((int)c.workers - 1));  // + the builder thread itself
+    b->workers.reset(new Pool((int)c.workers - 1));  // + the completion thread itself
     b->builder = std::thread([b] {
         (void)hipSetDevice(b->cfg.device);
         b->build_loop();
@@ -769,6 +774,7 @@ void cyaes_batcher_destroy(cyaes_batcher* b) {
                 B.copy_in * us / nb, B.submit * us / nb, C.sync * us / nb, C.copy_out * us / nb, C.callbacks * us / nb);
     }
     b->workers.reset();
+    b->in_pool.reset();
     int dev_prev = 0;
     (void)hipGetDevice(&dev_prev);
     (void)hipSetDevice(b->cfg.device);

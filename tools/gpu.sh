@@ -13,6 +13,7 @@
 #   batchertest  tests/test_batcher.py only
 #   batcher    build/bench_batcher SEAL / OPEN loads (host to host), zero-copy and bounce ($BB_ARGS appended)
 #   hostlink   build/hostlink: kernel-driven packet gather/scatter over PCIe vs DMA
+#   bb:ARGS    one build/bench_batcher run (ARGS comma-separated) with CYAES_BATCHER_PROFILE phases, to bb.txt
 #   ab:A:B[:ARGS]  tools/ab.py on variant libraries build/variants/{A,B}.so, both orders
 #                  (ARGS: extra ab.py arguments, commas for spaces)
 #   abrelay:A:B    tools/ab_relay_layout.py on the two variants (relay stream layouts)
@@ -59,6 +60,10 @@ for step in "$@"; do
         grep '^{' "$O/bench_batcher_one.txt" >> "$O/bench_batcher.jsonl"
       done ;;
     hostlink) run hostlink 240 build/hostlink ;;
+    bb:*)  # one bench_batcher run, arguments comma-separated: bb:--op,seal,--window,16384
+      A=${step#bb:}
+      CYAES_BATCHER_PROFILE=1 run bench_batcher_one 120 build/bench_batcher ${A//,/ } --threads ${BB_THREADS:-8} --seconds ${BB_SECONDS:-4}
+      { grep '^{' "$O/bench_batcher_one.txt" | tr -d '\n'; echo -n ', '; grep '^\[cyaes_batcher\]' "$O/bench_batcher_one.txt" || echo; } >> "$O/bb.txt" ;;
     ab:*)
       IFS=: read -r _ A B ARGS <<< "$step"
       L="build/variants/$A.so build/variants/$B.so"
