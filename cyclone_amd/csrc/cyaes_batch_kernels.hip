@@ -16,6 +16,8 @@
 //   k_batch_scatter: stage -> outputs: the sealed packet (SEAL), the payload
 //                    decrypted in place behind the untouched header (OPEN,
 //                    relay_server.cpp:329), or the CBC output (ENCRYPT/DECRYPT).
+#include <algorithm>
+
 #include "cyaes_internal.h"
 #include "cyaes_relay.h"
 
@@ -28,106 +30,132 @@ constexpr uint32_t kForwardId = CYAES_RELAY_FORWARD;       // relay_protocol.h:9
 constexpr uint8_t kPad = CYAES_RELAY_PAD;                  // Packet::_resize fill (cye_packet.cpp:102)
 
 // dst[0, n) = src[0, n), one wave: 16 B per lane when both ends and n are
-// 16-B aligned, else dwords when 4-B aligned (the tail bytes singly), else bytes.
+// 16-B aligned, else dwords when 4-B aligned (the tail bytes singly), else
+// bytes.  Each round issues all its loads before its stores (4 KiB of dwords
+// or 4 KiB of dwordx4 per wave), so a relay packet costs one or two PCIe round
+// trips instead of one per 256 B.
 __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t lane) {
     const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
     if (((a | n) & 15u) == 0) {
-        for (uint32_t o = 16 * lane; o < n; o += 1024)
-            *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(src + o);
+        for (uint32_t o0 = 0; o0 < n; o0 += 4096) {
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t o = o0 + 1024 * k + 16 * lane;
+                if (o < n) v[k] = *reinterpret_cast<const uint4*>(src + o);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t o = o0 + 1024 * k + 16 * lane;
+                if (o < n) *reinterpret_cast<uint4*>(dst + o) = v[k];
+            }
+        }
         return;
     }
     uint32_t body = 0;
     if ((a & 3u) == 0) {
         body = n & ~3u;
-        for (uint32_t o = 4 * lane; o < body; o += 256)
-            *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(src + o);
+        for (uint32_t o0 = 0; o0 < body; o0 += 4096) {
+            uint32_t v[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const uint32_t o = o0 + 256 * k + 4 * lane;
+                if (o < body) v[k] = *reinterpret_cast<const uint32_t*>(src + o);
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const uint32_t o = o0 + 256 * k + 4 * lane;
+                if (o < body) *reinterpret_cast<uint32_t*>(dst + o) = v[k];
+            }
+        }
     }
     for (uint32_t o = body + lane; o < n; o += 64) dst[o] = src[o];
 }
 
 __device__ __forceinline__ bool is_relay(uint32_t op) { return op >= kOpRelaySeal; }
 
-// One wave per request (grid-stride).  Requests [0, ne) are the encrypt list
-// (ENCRYPT, SEAL), [ne, n) the decrypt list (DECRYPT, OPEN); list entry i of
-// the ragged kernels is request i (the decrypt kernel gets the lists from ne).
-__global__ void k_batch_gather(const BatchDesc* __restrict__ desc, uint32_t n, uint8_t* __restrict__ stage,
-                               uint64_t* __restrict__ offs, uint32_t* __restrict__ nbytes, uint32_t* __restrict__ kidx) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nw = gridDim.x * (blockDim.x / 64);
-    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nw) {
-        const BatchDesc d = desc[i];
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(d.src);
-        uint8_t* s = stage + d.stage;
-        if (lane == 0) {
-            offs[i] = is_relay(d.op) ? d.stage + 16 : d.stage;  // relay payload 16-B aligned at stage + 16
-            nbytes[i] = d.crypt;
-            kidx[i] = d.key;
-        }
-        switch (d.op) {
-            case kOpEncrypt:
-            case kOpDecrypt:
-                wave_copy(s, src, d.size, lane);
-                break;
-            case kOpRelaySeal: {  // packet at stage + 4, so its payload (offset 12) is at stage + 16
-                uint8_t* pk = s + kHead;
-                if (lane == 0) {
-                    const uint32_t psize = 8 + d.crypt;
-                    pk[0] = (uint8_t)(psize >> 8);
-                    pk[1] = (uint8_t)psize;
-                    pk[2] = (uint8_t)(kForwardId >> 8);
-                    pk[3] = (uint8_t)kForwardId;
-                    *reinterpret_cast<int32_t*>(pk + 4) = d.conn;          // RelayForwardMsg::id
-                    *reinterpret_cast<int32_t*>(pk + 8) = (int32_t)d.size; // RelayForwardMsg::size
-                }
-                wave_copy(pk + kPayload, src, d.size, lane);
-                for (uint32_t o = d.size + lane; o < d.crypt; o += 64) pk[kPayload + o] = kPad;
-                break;
+// Gather of request i: input -> stage, and the ragged kernels' list entry i.
+// Requests [0, ne) are the encrypt list (ENCRYPT, SEAL), [ne, n) the decrypt
+// list (DECRYPT, OPEN); the decrypt kernel gets the lists from ne.
+__device__ __forceinline__ void gather_one(const BatchDesc& d, uint32_t i, uint8_t* __restrict__ stage,
+                                           uint64_t* __restrict__ offs, uint32_t* __restrict__ nbytes,
+                                           uint32_t* __restrict__ kidx, uint32_t lane) {
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(d.src);
+    uint8_t* s = stage + d.stage;
+    if (lane == 0) {
+        offs[i] = is_relay(d.op) ? d.stage + 16 : d.stage;  // relay payload 16-B aligned at stage + 16
+        nbytes[i] = d.crypt;
+        kidx[i] = d.key;
+    }
+    switch (d.op) {
+        case kOpEncrypt:
+        case kOpDecrypt:
+            wave_copy(s, src, d.size, lane);
+            break;
+        case kOpRelaySeal: {  // packet at stage + 4, so its payload (offset 12) is at stage + 16
+            uint8_t* pk = s + kHead;
+            if (lane == 0) {
+                const uint32_t psize = 8 + d.crypt;
+                pk[0] = (uint8_t)(psize >> 8);
+                pk[1] = (uint8_t)psize;
+                pk[2] = (uint8_t)(kForwardId >> 8);
+                pk[3] = (uint8_t)kForwardId;
+                *reinterpret_cast<int32_t*>(pk + 4) = d.conn;          // RelayForwardMsg::id
+                *reinterpret_cast<int32_t*>(pk + 8) = (int32_t)d.size; // RelayForwardMsg::size
             }
-            case kOpRelayOpen:  // the payload only: the header stays where it is
-                wave_copy(s + 16, src + kPayload, d.crypt, lane);
-                break;
+            wave_copy(pk + kPayload, src, d.size, lane);
+            for (uint32_t o = d.size + lane; o < d.crypt; o += 64) pk[kPayload + o] = kPad;
+            break;
         }
+        case kOpRelayOpen:  // the payload only: the header stays where it is
+            wave_copy(s + 16, src + kPayload, d.crypt, lane);
+            break;
     }
 }
 
-__global__ void k_batch_scatter(const BatchDesc* __restrict__ desc, uint32_t n, const uint8_t* __restrict__ stage) {
+__device__ __forceinline__ void scatter_one(const BatchDesc& d, const uint8_t* __restrict__ stage, uint32_t lane) {
+    uint8_t* dst = reinterpret_cast<uint8_t*>(d.dst);
+    const uint8_t* s = stage + d.stage;
+    switch (d.op) {
+        case kOpEncrypt:
+        case kOpDecrypt:
+            wave_copy(dst, s, d.size, lane);
+            break;
+        case kOpRelaySeal:  // the whole packet: header, RelayForwardMsg, ciphertext
+            wave_copy(dst, s + kHead, kPayload + d.crypt, lane);
+            break;
+        case kOpRelayOpen:  // plaintext back behind the header (in place)
+            wave_copy(dst + kPayload, s + 16, d.crypt, lane);
+            break;
+    }
+}
+
+// One launch moves both PCIe directions: the scatter of batch k (its outputs,
+// stage -> host pools) and the gather of batch k+1 (inputs, host pools ->
+// stage), so the batcher's single in-order pipeline stream keeps H2D and D2H
+// busy at once.  The waves split between the two lists in proportion to
+// their request counts; one wave per request, grid-stride.
+__global__ void k_batch_move(BatchMove m) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * (blockDim.x / 64);
-    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nw) {
-        const BatchDesc d = desc[i];
-        uint8_t* dst = reinterpret_cast<uint8_t*>(d.dst);
-        const uint8_t* s = stage + d.stage;
-        switch (d.op) {
-            case kOpEncrypt:
-            case kOpDecrypt:
-                wave_copy(dst, s, d.size, lane);
-                break;
-            case kOpRelaySeal:  // the whole packet: header, RelayForwardMsg, ciphertext
-                wave_copy(dst, s + kHead, kPayload + d.crypt, lane);
-                break;
-            case kOpRelayOpen:  // plaintext back behind the header (in place)
-                wave_copy(dst + kPayload, s + 16, d.crypt, lane);
-                break;
-        }
+    const uint32_t w = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const uint64_t tot = (uint64_t)m.gn + m.sn;
+    const uint32_t gw = m.sn == 0 ? nw : m.gn == 0 ? 0 : (uint32_t)max<uint64_t>(1, min<uint64_t>(nw - 1, nw * m.gn / tot));
+    if (w < gw) {
+        for (uint32_t i = w; i < m.gn; i += gw) gather_one(m.gdesc[i], i, m.gstage, m.offs, m.nbytes, m.kidx, lane);
+    } else {
+        const uint32_t sw = nw - gw;
+        for (uint32_t i = w - gw; i < m.sn; i += sw) scatter_one(m.sdesc[i], m.sstage, lane);
     }
 }
 
 }  // namespace
 
-hipError_t launch_batch_gather(const BatchDesc* d_desc, uint32_t n, uint8_t* d_stage, uint64_t* d_offs,
-                               uint32_t* d_nbytes, uint32_t* d_kidx, int max_waves, hipStream_t stream) {
+hipError_t launch_batch_move(const BatchMove& m, int max_waves, hipStream_t stream) {
+    const uint64_t n = (uint64_t)m.gn + m.sn;
     if (n == 0) return hipSuccess;
-    const uint32_t waves = n < (uint32_t)max_waves ? n : (uint32_t)max_waves;
-    hipLaunchKernelGGL(k_batch_gather, dim3((waves + 3) / 4), dim3(256), 0, stream, d_desc, n, d_stage, d_offs,
-                       d_nbytes, d_kidx);
-    return hipGetLastError();
-}
-
-hipError_t launch_batch_scatter(const BatchDesc* d_desc, uint32_t n, const uint8_t* d_stage, int max_waves,
-                                hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    const uint32_t waves = n < (uint32_t)max_waves ? n : (uint32_t)max_waves;
-    hipLaunchKernelGGL(k_batch_scatter, dim3((waves + 3) / 4), dim3(256), 0, stream, d_desc, n, d_stage);
+    const uint32_t waves = (uint32_t)std::min<uint64_t>(n, (uint64_t)std::max(2, max_waves));
+    hipLaunchKernelGGL(k_batch_move, dim3((waves + 3) / 4), dim3(256), 0, stream, m);
     return hipGetLastError();
 }
 

@@ -20,12 +20,17 @@
 //    the close has completed (per-shard completion watermarks), so requests
 //    already submitted keep their key.
 //  * Submitters append descriptors to their thread's shard (one short lock per
-//    submit call); the builder swaps the shard queues out, lays the batch out
-//    with a few stores per request (encrypt-type descriptors first, then
-//    decrypt-type, so each direction is one ragged list), one H2D of the
-//    descriptors, and four kernels on the stage's stream; the completion
-//    thread waits for the stage and runs the callbacks, one job per shard on
-//    the worker pool, each shard's callbacks in its submission order.
+//    submit call); the builder swaps the shard queues out and lays the batch
+//    out with a few stores per request (encrypt-type descriptors first, then
+//    decrypt-type, so each direction is one ragged list).
+//  * One in-order pipeline stream (streams sharing a hardware queue serialise
+//    anyway): H2D of batch k+1's descriptors; one move kernel that scatters
+//    batch k's outputs while it gathers batch k+1's inputs, so both PCIe
+//    directions run at once; batch k's completion event; batch k+1's AES
+//    kernels, alone on the GPU.  An idle builder flushes the last scatter.
+//  * The completion thread waits for each batch's event and runs the
+//    callbacks, one job per shard on the worker pool, each shard's callbacks
+//    in its submission order.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -71,6 +76,7 @@ constexpr uint32_t kMaxReqs = 65536;   // requests per batch
 constexpr int kMaxPools = 64;
 constexpr uint32_t kNoRow = ~0u;
 constexpr uint32_t kSchedBytes = cyaes::kSchedWords * 4;
+constexpr size_t kCopyChunk = 64;      // bounce copies per worker job (one atomic per chunk, not per copy)
 
 // Stage bytes of a request's data in HBM: relay packets keep their payload at
 // stage + 16 (16-B aligned), with the packet's 12 header bytes before it.
@@ -222,8 +228,7 @@ struct Stage {
     uint64_t* d_offs = nullptr;
     uint32_t *d_nb = nullptr, *d_kid = nullptr;
     uint8_t* d_data = nullptr;
-    hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;
+    hipEvent_t done = nullptr;  // recorded after the batch's scatter
     uint32_t ne = 0, nd = 0;
     uint64_t bytes = 0;  // payload bytes en/decrypted (stats)
     std::vector<Cb> cbs;
@@ -243,8 +248,10 @@ struct cyaes_batcher {
     cyaes_batcher_config cfg{};
     cyaes_gpu* ctx = nullptr;
     uint64_t data_cap = 0, bounce_cap = 0;
-    int gather_waves = 0;
+    int move_waves = 0;
     std::vector<Stage> stages;
+    hipStream_t pipe = nullptr;  // the device pipeline (builder thread only)
+    Stage* pending = nullptr;    // launched, its scatter not yet (builder thread only)
 
     std::array<Shard, kShards> shards;
     std::atomic<int64_t> queued_reqs{0}, queued_bytes{0};
@@ -295,6 +302,8 @@ struct cyaes_batcher {
     void build_loop();
     void complete_loop();
     int launch(Stage* st);
+    void flush_pending();
+    void hand_off(Stage* st);
     int wait_enqueued(const std::array<uint64_t, kShards>& target);
 };
 
@@ -451,6 +460,20 @@ void cyaes_batcher::build_loop() {
         for (int s = 0; s < kShards && !have; s++) have = ppos[s] < pend[s].size();
         {
             std::unique_lock<std::mutex> lk(mu);
+            if (!have && pending) {
+                // The last batch's scatter rides on the next batch's move kernel;
+                // with nothing queued for a short while (or a flush / stop), send
+                // it alone.
+                const auto until = Clock::now() + std::chrono::microseconds(std::min<uint32_t>(cfg.max_delay_us, 50));
+                if (!cv_submit.wait_until(lk, until, [&] { return queued_reqs.load() > 0; }) || stop ||
+                    flushers.load() > 0) {
+                    if (queued_reqs.load() <= 0) {
+                        lk.unlock();
+                        flush_pending();
+                        continue;
+                    }
+                }
+            }
             if (!have) {
                 cv_submit.wait(lk, [&] { return stop || queued_reqs.load() > 0; });
                 if (queued_reqs.load() <= 0) break;  // stop requested and drained
@@ -460,6 +483,11 @@ void cyaes_batcher::build_loop() {
                 cv_submit.wait_until(lk, due, [&] {
                     return stop || flushers.load() > 0 || queued_bytes.load() >= (int64_t)cfg.max_batch_bytes;
                 });
+            }
+            if (free_stages.empty() && pending) {  // every stage in flight: the pending one must drain
+                lk.unlock();
+                flush_pending();
+                lk.lock();
             }
             cv_free.wait(lk, [&] { return !free_stages.empty(); });
             st = free_stages.back();
@@ -558,45 +586,74 @@ void cyaes_batcher::build_loop() {
             free_stages.push_back(st);
             continue;
         }
-        in_pool->run(copies.size(), [&](size_t i) {
-            memcpy(const_cast<uint8_t*>(copies[i][0]), copies[i][1], (size_t)(uintptr_t)copies[i][2]);
+        in_pool->run((copies.size() + kCopyChunk - 1) / kCopyChunk, [&](size_t c) {
+            for (size_t i = c * kCopyChunk; i < std::min(copies.size(), (c + 1) * kCopyChunk); i++)
+                memcpy(const_cast<uint8_t*>(copies[i][0]), copies[i][1], (size_t)(uintptr_t)copies[i][2]);
         });
         const int64_t ts = now_ns();
         pb.copy_in += ts - tc;
         st->status = launch(st);
         pb.submit += now_ns() - ts;
-        std::lock_guard<std::mutex> lk(mu);
-        inflight.push_back(st);
-        cv_inflight.notify_one();
     }
+    flush_pending();
     std::lock_guard<std::mutex> lk(mu);
     builder_done = true;
     cv_inflight.notify_all();
 }
 
-// One H2D of the descriptors, then gather -> encrypt -> decrypt -> scatter on
-// the stage's stream (cyaes_batch_kernels.hip, cyaes_kernels.hip).
+// To the completion thread, in launch order.
+void cyaes_batcher::hand_off(Stage* st) {
+    std::lock_guard<std::mutex> lk(mu);
+    inflight.push_back(st);
+    cv_inflight.notify_one();
+}
+
+// The pending batch's scatter on its own move kernel.
+void cyaes_batcher::flush_pending() {
+    Stage* p = pending;
+    if (!p) return;
+    pending = nullptr;
+    if (p->status == CYAES_OK) {  // (a failed batch is not scattered: its outputs would be garbage)
+        cyaes::BatchMove m{};
+        m.sdesc = p->d_desc;
+        m.sn = p->ne + p->nd;
+        m.sstage = p->d_data;
+        hipError_t e = cyaes::launch_batch_move(m, move_waves, pipe);
+        if (e == hipSuccess) e = hipEventRecord(p->done, pipe);
+        p->status = map_err(e);
+    }
+    hand_off(p);
+}
+
+// On the pipeline stream: H2D of the descriptors; one move kernel gathering
+// this batch and scattering the pending one (whose completion event follows);
+// then this batch's encrypt and decrypt kernels.  This batch becomes pending.
 int cyaes_batcher::launch(Stage* st) {
     const uint32_t ne = st->ne, nd = st->nd, n = ne + nd;
+    Stage* prev = pending;
+    pending = nullptr;
     hipError_t e = hipSuccess;
-    if (ne) e = hipMemcpyAsync(st->d_desc, st->h_enc, ne * sizeof(BatchDesc), hipMemcpyHostToDevice, st->stream);
+    if (ne) e = hipMemcpyAsync(st->d_desc, st->h_enc, ne * sizeof(BatchDesc), hipMemcpyHostToDevice, pipe);
     if (e == hipSuccess && nd)
-        e = hipMemcpyAsync(st->d_desc + ne, st->h_dec, nd * sizeof(BatchDesc), hipMemcpyHostToDevice, st->stream);
-    if (e == hipSuccess)
-        e = cyaes::launch_batch_gather(st->d_desc, n, st->d_data, st->d_offs, st->d_nb, st->d_kid, gather_waves,
-                                       st->stream);
-    if (e != hipSuccess) return map_err(e);
-    int rc = CYAES_OK;
-    if (ne)
+        e = hipMemcpyAsync(st->d_desc + ne, st->h_dec, nd * sizeof(BatchDesc), hipMemcpyHostToDevice, pipe);
+    const bool sc = prev && prev->status == CYAES_OK;  // (a failed batch is not scattered)
+    cyaes::BatchMove m{st->d_desc, n, sc ? prev->ne + prev->nd : 0u, st->d_data, st->d_offs, st->d_nb, st->d_kid,
+                       sc ? prev->d_desc : nullptr, sc ? prev->d_data : nullptr};
+    if (e == hipSuccess) e = cyaes::launch_batch_move(m, move_waves, pipe);
+    if (prev) {
+        if (sc && e == hipSuccess) e = hipEventRecord(prev->done, pipe);
+        if (sc) prev->status = map_err(e);
+        hand_off(prev);
+    }
+    int rc = map_err(e);
+    if (rc == CYAES_OK && ne)
         rc = cyaes::ragged_batch(ctx, false, d_keys, key_cap, st->d_data, st->d_data, st->d_offs, st->d_nb, ne,
-                                 st->d_kid, st->stream);
+                                 st->d_kid, pipe);
     if (rc == CYAES_OK && nd)
         rc = cyaes::ragged_batch(ctx, true, d_keys, key_cap, st->d_data, st->d_data, st->d_offs + ne, st->d_nb + ne,
-                                 nd, st->d_kid + ne, st->stream);
-    if (rc != CYAES_OK) return rc;
-    e = cyaes::launch_batch_scatter(st->d_desc, n, st->d_data, gather_waves, st->stream);
-    if (e == hipSuccess) e = hipEventRecord(st->done, st->stream);
-    return map_err(e);
+                                 nd, st->d_kid + ne, pipe);
+    pending = st;  // (a failed batch still goes through flush / the next launch, with its status)
+    return rc;
 }
 
 // ---- completion ------------------------------------------------------------
@@ -612,14 +669,14 @@ void cyaes_batcher::complete_loop() {
         const int64_t t0 = now_ns();
         if (status == CYAES_OK) status = map_err(hipEventSynchronize(st->done));
         // A stage whose launch failed part-way may still have work in flight on
-        // its buffers: drain its stream before the stage is reused.
-        if (status != CYAES_OK) (void)hipStreamSynchronize(st->stream);
+        // its buffers: drain the pipeline before the stage is reused.
+        if (status != CYAES_OK) (void)hipStreamSynchronize(pipe);
         const int64_t t1 = now_ns();
         pc.sync += t1 - t0;
         if (status == CYAES_OK)
-            workers->run(st->bouts.size(), [st](size_t i) {
-                const BounceOut& b = st->bouts[i];
-                memcpy(b.to, b.from, b.bytes);
+            workers->run((st->bouts.size() + kCopyChunk - 1) / kCopyChunk, [st](size_t c) {
+                for (size_t i = c * kCopyChunk; i < std::min(st->bouts.size(), (c + 1) * kCopyChunk); i++)
+                    memcpy(st->bouts[i].to, st->bouts[i].from, st->bouts[i].bytes);
             });
         const int64_t t2 = now_ns();
         pc.copy_out += t2 - t1;
@@ -699,7 +756,10 @@ int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out) {
     // always taken; submit caps a request at max_batch_bytes).
     b->data_cap = (uint64_t)c.max_batch_bytes;
     b->bounce_cap = (uint64_t)c.max_batch_bytes + 2 * 65536;
-    b->gather_waves = std::max(64, cyaes_gpu_num_cus(ctx) * 32);
+    // Move-kernel waves (one request each at a time, split between the two
+    // directions): enough packets in flight to cover PCIe latency both ways.
+    b->move_waves = std::max(64, cyaes_gpu_num_cus(ctx) * 8);
+    if (const char* w = getenv("CYAES_BATCH_COPY_WAVES")) b->move_waves = std::max(2, atoi(w));  // A/B
     b->key_cap = c.max_sessions;
     b->stages.resize(c.inflight);
     int dev_prev = 0;
@@ -728,13 +788,13 @@ int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out) {
             s.d_nb = reinterpret_cast<uint32_t*>(s.d_offs + kMaxReqs);
             s.d_kid = s.d_nb + kMaxReqs;
             s.d_data = reinterpret_cast<uint8_t*>(s.d_kid + kMaxReqs);
-            e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
         }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
         s.cbs.reserve(kMaxReqs);
         b->free_stages.push_back(&s);
     }
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&b->d_keys), (uint64_t)b->key_cap * kSchedBytes);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->pipe, hipStreamNonBlocking);
     (void)hipSetDevice(dev_prev);
     if (e != hipSuccess) {
         b->builder_done = true;
@@ -778,15 +838,15 @@ void cyaes_batcher_destroy(cyaes_batcher* b) {
     int dev_prev = 0;
     (void)hipGetDevice(&dev_prev);
     (void)hipSetDevice(b->cfg.device);
+    if (b->pipe) (void)hipStreamSynchronize(b->pipe);
     for (Stage& s : b->stages) {
-        if (s.stream) (void)hipStreamSynchronize(s.stream);
         if (s.done) (void)hipEventDestroy(s.done);
-        if (s.stream) (void)hipStreamDestroy(s.stream);
         if (s.d_mem) (void)hipFree(s.d_mem);
         if (s.h_enc) (void)hipHostFree(s.h_enc);
         if (s.h_bounce) (void)hipHostFree(s.h_bounce);
     }
     if (b->d_keys) (void)hipFree(b->d_keys);
+    if (b->pipe) (void)hipStreamDestroy(b->pipe);
     for (PoolEnt& p : b->pools)
         if (p.live && p.owned) (void)hipHostUnregister(p.pinned);
     (void)hipSetDevice(dev_prev);

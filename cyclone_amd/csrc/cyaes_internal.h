@@ -87,6 +87,7 @@ struct EncArgs {
     uint8_t* iv_out;
     const uint32_t* tables;  // kEncTableWords
     uint32_t* status;
+    uint32_t run;            // uniform lane kernel: payloads per work item (> 1: k_encrypt RUNS; no IV arrays)
 };
 
 struct DecArgs {
@@ -140,10 +141,20 @@ struct BatchDesc {
     uint32_t stage;  // byte offset of the request's data in the batch's HBM stage
 };
 static_assert(sizeof(BatchDesc) == 40, "BatchDesc layout");
-hipError_t launch_batch_gather(const BatchDesc* d_desc, uint32_t n, uint8_t* d_stage, uint64_t* d_offs,
-                               uint32_t* d_nbytes, uint32_t* d_kidx, int max_waves, hipStream_t stream);
-hipError_t launch_batch_scatter(const BatchDesc* d_desc, uint32_t n, const uint8_t* d_stage, int max_waves,
-                                hipStream_t stream);
+// One kernel for both PCIe directions of the batcher's pipeline: gather of
+// one batch (gdesc[0, gn) into gstage, plus the ragged lists offs / nbytes /
+// kidx) and scatter of the previous one (sdesc[0, sn) out of sstage).
+struct BatchMove {
+    const BatchDesc* gdesc;
+    uint32_t gn, sn;
+    uint8_t* gstage;
+    uint64_t* offs;
+    uint32_t* nbytes;
+    uint32_t* kidx;
+    const BatchDesc* sdesc;
+    const uint8_t* sstage;
+};
+hipError_t launch_batch_move(const BatchMove& m, int max_waves, hipStream_t stream);
 
 // Host runtime (cyaes_runtime.cpp): ragged batch under an explicit device key
 // table of table_keys schedules (the batcher's per-batch session keys).

@@ -398,7 +398,15 @@ struct ClockProbe {
 __device__ __forceinline__ void drain_loads() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---- CBC encrypt: one lane per payload chain (cyr_rijndael.cpp:588-609) ----
-template <bool RAGGED, bool KEYED>
+// RUNS (uniform batches of short payloads, no IV arrays): a lane's work item
+// is a run of a.run consecutive payloads, contiguous in memory, encrypted as
+// one block stream whose chain restarts at DefaultIV every bpp blocks
+// (relay_local.cpp:206 passes no IV, so every payload is its own chain).  The
+// next-chunk prefetch then never stops at a payload boundary: a lane of
+// config B (1,472-B payloads) streams 368 blocks instead of four 92-block
+// payloads, each of which started on an exposed load and ended in a 4-block
+// tail.  The restart test is on wave-uniform block counters (scalar).
+template <bool RAGGED, bool KEYED, bool RUNS>
 __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
     fill_region(lds_words, a.tables, a.tables + 512, blockDim.x);              // TL1 | TL3
@@ -416,10 +424,16 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     const uint64_t wstride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t wbase0 = (uint64_t)blockIdx.x * blockDim.x + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
     const Ext iv_in_e = iv_ext(a.iv_in, a.npayloads), iv_out_e = iv_ext(a.iv_out, a.npayloads);
+    const uint32_t R = RUNS ? a.run : 1u;  // payloads per work item
+    const uint32_t bpp = a.payload_bytes >> 4;
+    const uint64_t nwork = RUNS ? (a.npayloads + R - 1) / R : a.npayloads;
+    uint32_t ek[44];
+    if (!KEYED) load_sched(a.keys, 0, 0, ek);  // one schedule for the whole batch
 
-    for (uint64_t wbase = wbase0; wbase < a.npayloads; wbase += wstride) {
-        const uint64_t p = wbase + lane;
-        const bool active = p < a.npayloads;
+    for (uint64_t wbase = wbase0; wbase < nwork; wbase += wstride) {
+        const uint64_t w = wbase + lane;
+        const bool active = w < nwork;
+        const uint64_t p = RUNS ? w * R : w;  // (first) payload of the work item
         uint64_t off;
         uint32_t nb;
         if (RAGGED) {
@@ -427,8 +441,9 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
             nb = active ? (LD4(a.nbytes + p, ext(a.nbytes, 4 * a.npayloads)) >> 4) : 0;
         } else {
             off = p * (uint64_t)a.payload_bytes;
-            nb = active ? (a.payload_bytes >> 4) : 0;
+            nb = active ? (RUNS ? (uint32_t)min<uint64_t>(R, a.npayloads - p) * bpp : bpp) : 0;
         }
+        // RUNS + KEYED: the runtime makes runs divide payloads_per_key, so the run is one session
         const uint32_t kid = KEYED ? key_index(a.keys, p, a.npayloads, active, a.status) : 0u;
         bool pending = active;
         while (true) {  // waterfall over the distinct keys of this wave
@@ -437,12 +452,12 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
             const uint32_t ku = KEYED ? __builtin_amdgcn_readlane(kid, __builtin_ctzll(m)) : 0u;
             if (pending && (!KEYED || kid == ku)) {
                 pending = false;
-                uint32_t ek[44];
-                load_sched(a.keys, ku, 0, ek);
+                if (KEYED) load_sched(a.keys, ku, 0, ek);
                 uint4 c = a.iv_in ? LD16(a.iv_in + 16 * p, iv_in_e) : default_iv();
                 const uint8_t* src = a.in + off;  // ragged: 4-B aligned
                 uint8_t* dst = a.out + off;
-                const Ext se = ext(src, 16ull * nb), de = ext(dst, 16ull * nb);  // this payload's bytes
+                const Ext se = ext(src, 16ull * nb), de = ext(dst, 16ull * nb);  // this work item's bytes
+                uint32_t nr = bpp;  // RUNS: block index of the next chain restart (a payload start)
                 uint32_t i = 0;
                 uint4 b[8];
                 if (nb >= 8) {
@@ -469,6 +484,10 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                     prio_feedback(&lead, ++prog, kEncPrioDiv);
 #pragma unroll
                     for (int j = 0; j < 8; j++) {
+                        if (RUNS && i + j == nr) {  // next payload of the run: a new chain
+                            c = default_iv();
+                            nr += bpp;
+                        }
                         uint32_t s0 = xor3(c.x, b[j].x, ek[0]), s1 = xor3(c.y, b[j].y, ek[1]);
                         uint32_t s2 = xor3(c.z, b[j].z, ek[2]), s3 = xor3(c.w, b[j].w, ek[3]);
                         enc_block(lds, lo, ek, s0, s1, s2, s3);
@@ -497,13 +516,17 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                     const uint4 v = have_tail ? b[0] : ldb<RAGGED>(src, i, se);
 #pragma unroll
                     for (int j = 0; j < 7; j++) b[j] = b[j + 1];
+                    if (RUNS && i == nr) {
+                        c = default_iv();
+                        nr += bpp;
+                    }
                     uint32_t s0 = xor3(c.x, v.x, ek[0]), s1 = xor3(c.y, v.y, ek[1]);
                     uint32_t s2 = xor3(c.z, v.z, ek[2]), s3 = xor3(c.w, v.w, ek[3]);
                     enc_block(lds, lo, ek, s0, s1, s2, s3);
                     c = make_uint4(s0, s1, s2, s3);
                     stb<RAGGED>(dst, i, c, de);
                 }
-                if (a.iv_out) ST16(a.iv_out + 16 * p, iv_out_e, c);
+                if (a.iv_out) ST16(a.iv_out + 16 * p, iv_out_e, c);  // (RUNS: no IV arrays)
             }
         }
     }
@@ -1194,10 +1217,13 @@ hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t s
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
     const bool ragged = a.offsets != nullptr;
     const dim3 g(grid), b(threads);
-    if (ragged && keyed) hipLaunchKernelGGL((k_encrypt<true, true>), g, b, 0, stream, a);
-    else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false>), g, b, 0, stream, a);
-    else if (keyed) hipLaunchKernelGGL((k_encrypt<false, true>), g, b, 0, stream, a);
-    else hipLaunchKernelGGL((k_encrypt<false, false>), g, b, 0, stream, a);
+    const bool runs = !ragged && a.run > 1;
+    if (ragged && keyed) hipLaunchKernelGGL((k_encrypt<true, true, false>), g, b, 0, stream, a);
+    else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false, false>), g, b, 0, stream, a);
+    else if (runs && keyed) hipLaunchKernelGGL((k_encrypt<false, true, true>), g, b, 0, stream, a);
+    else if (runs) hipLaunchKernelGGL((k_encrypt<false, false, true>), g, b, 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_encrypt<false, true, false>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((k_encrypt<false, false, false>), g, b, 0, stream, a);
     return hipGetLastError();
 }
 

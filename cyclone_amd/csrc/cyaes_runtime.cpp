@@ -22,6 +22,7 @@ struct cyaes_gpu {
     int num_cus = 0;
     uint64_t quad_max_chains = CYAES_QUAD_MAX_CHAINS;  // env CYAES_QUAD_MAX_CHAINS (A/B only)
     uint32_t ragged_group = 0;  // env CYAES_RAGGED_GROUP: payloads per ragged-decrypt wave group (0 = auto; tests, A/B)
+    uint32_t enc_run = 0;       // env CYAES_ENC_RUN: payloads per lane run of the uniform encrypt (0 = auto; tests, A/B)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
     uint32_t* d_keys = nullptr;    // nkeys * kSchedWords
     uint32_t nkeys = 0;
@@ -83,6 +84,9 @@ int make_keysel(const cyaes_gpu* ctx, uint64_t npayloads, const uint32_t* key_id
     return CYAES_OK;
 }
 
+constexpr uint64_t kRunMax = 8;               // payloads per encrypt run
+constexpr uint32_t kRunMaxPayload = 8192;      // runs only for payloads up to 512 blocks
+
 int enc_grid_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kEncWgPerCu); }
 int dec_grid_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kDecWgPerCu); }
 
@@ -134,7 +138,21 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
         const Shape sh = wave_shape(ctx, (4 * npayloads + 63) / 64, kEncThreads);
         return map_err(launch_encrypt_quad(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
     }
-    const Shape sh = wave_shape(ctx, (npayloads + 63) / 64, kEncThreads);
+    // Runs (k_encrypt RUNS): a uniform batch of short payloads with more
+    // payloads than the chip has lanes gives each lane R consecutive payloads
+    // as one block stream (contiguous, so the chunk prefetch never stops at a
+    // payload start), with R payloads per lane-chain still leaving >= one work
+    // item per lane; sessions must hold whole runs.
+    uint64_t R = 1;
+    if (!offsets && !iv_in && !iv_out && !key_idx && payload_bytes <= kRunMaxPayload) {
+        const uint64_t lanes = (uint64_t)std::max(1, ctx->num_cus) * kEncThreads;
+        R = std::min<uint64_t>(kRunMax, npayloads / lanes);
+        while (R > 1 && ppk % R) R--;
+    }
+    if (ctx->enc_run) R = ctx->enc_run;  // A/B override (env CYAES_ENC_RUN)
+    if (offsets || iv_in || iv_out || key_idx || (ppk && ppk % R)) R = 1;
+    a.run = (uint32_t)std::max<uint64_t>(1, R);
+    const Shape sh = wave_shape(ctx, ((npayloads + a.run - 1) / a.run + 63) / 64, kEncThreads);
     return map_err(launch_encrypt(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
 }
 
@@ -317,6 +335,7 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     ctx->num_cus = prop.multiProcessorCount;
     if (const char* q = getenv("CYAES_QUAD_MAX_CHAINS")) ctx->quad_max_chains = strtoull(q, nullptr, 10);
     if (const char* g = getenv("CYAES_RAGGED_GROUP")) ctx->ragged_group = (uint32_t)strtoul(g, nullptr, 10);
+    if (const char* r = getenv("CYAES_ENC_RUN")) ctx->enc_run = (uint32_t)strtoul(r, nullptr, 10);
     const HostTables& t = host_tables();
     uint8_t host[kTablesBytes];
     memcpy(host + kEncTableOff, t.enc, sizeof(t.enc));

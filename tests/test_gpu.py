@@ -28,24 +28,30 @@ def torch():
 # Encrypt has two kernels: four lanes per chain for batches
 # under CYAES_QUAD_MAX_CHAINS chains (every small test batch here), one lane
 # per chain above.  "lane" forces the latter, so both run every test's paths
-# (keys, IVs, ragged, in place); the full-size configs below use it anyway.
-KERNEL_MODES = {"auto": None, "lane": "0"}
+# (keys, IVs, ragged, in place); "run3" also makes each lane's work item a run
+# of 3 consecutive payloads (k_encrypt RUNS, CYAES_ENC_RUN; the runtime keeps
+# single payloads where runs do not apply: IV arrays, key index arrays,
+# sessions that are not whole runs).  The full-size configs below use the
+# runtime's own choice.
+KERNEL_MODES = {"auto": {}, "lane": {"CYAES_QUAD_MAX_CHAINS": "0"},
+                "run3": {"CYAES_QUAD_MAX_CHAINS": "0", "CYAES_ENC_RUN": "3"}}
+_MODE_VARS = ("CYAES_QUAD_MAX_CHAINS", "CYAES_ENC_RUN")
 
 
 def _set_mode(mode):
-    old = os.environ.get("CYAES_QUAD_MAX_CHAINS")
-    if KERNEL_MODES[mode] is None:
-        os.environ.pop("CYAES_QUAD_MAX_CHAINS", None)
-    else:
-        os.environ["CYAES_QUAD_MAX_CHAINS"] = KERNEL_MODES[mode]
+    old = {k: os.environ.get(k) for k in _MODE_VARS}
+    for k in _MODE_VARS:
+        os.environ.pop(k, None)
+    os.environ.update(KERNEL_MODES[mode])
     return old
 
 
 def _restore(old):
-    if old is None:
-        os.environ.pop("CYAES_QUAD_MAX_CHAINS", None)
-    else:
-        os.environ["CYAES_QUAD_MAX_CHAINS"] = old
+    for k, v in old.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 
 
 @pytest.fixture(params=sorted(KERNEL_MODES))

@@ -4,6 +4,9 @@
 
 usage: python tools/ab.py build/variants/a.so build/variants/b.so [--rounds 6] [--payloads N]
        [--payload-bytes B] [--ppk K]   (--ppk: sessions of K payloads, config D's keys)
+A library may carry context settings: path:NAME=VALUE[:NAME=VALUE] sets those
+environment variables while its context is created (e.g. the same library
+twice, once with CYAES_ENC_RUN=1).
 Each round runs every variant's encrypt and decrypt once on the same config-C
 buffers; prints per-variant median/min ms per kernel and checks the outputs agree.
 """
@@ -31,9 +34,20 @@ def main():
     n, pb = args.payloads, args.payload_bytes
     nbytes = n * pb
     ctxs = []
-    for path in args.libs:
+    for spec in args.libs:
+        path, *envs = spec.split(":")
+        saved = {}
+        for kv in envs:
+            k, v = kv.split("=", 1)
+            saved[k] = os.environ.get(k)
+            os.environ[k] = v
         lib = ca.load_library(os.path.abspath(path))
         c = ca.GpuContext(0, lib=lib)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         if args.ppk:
             import bench
             c.set_keys(bench.session_keys((args.payloads + args.ppk - 1) // args.ppk))
@@ -48,7 +62,7 @@ def main():
     kidx = None
     if args.key_idx and args.ppk:
         kidx = (torch.arange(n, dtype=torch.int64, device="cuda") // args.ppk).to(torch.int32)
-    times = {p: {"enc": [], "dec": []} for p in args.libs}
+    times = {p: {"enc": [], "dec": []} for p in args.libs}  # keyed by spec
     probes = {}
     digests = {}
     for r in range(args.rounds + 1):
@@ -73,7 +87,7 @@ def main():
     for path in args.libs:
         t = times[path]
         print("%-40s enc med %.3f min %.3f | dec med %.3f min %.3f | %s" % (
-            os.path.basename(path), statistics.median(t["enc"]), min(t["enc"]), statistics.median(t["dec"]),
+            path.replace(ROOT + "/", "").replace("cyclone_amd/", ""), statistics.median(t["enc"]), min(t["enc"]), statistics.median(t["dec"]),
             min(t["dec"]), "same-output" if digests[path] == ref else "OUTPUT DIFFERS"))
         for kind, v in zip(("enc", "dec"), zip(*probes.get(path, []))):
             cyc, tick, waves, tmax = (sum(x[i] for x in v) for i in range(4))

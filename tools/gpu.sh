@@ -17,6 +17,7 @@
 #   ab:A:B[:ARGS]  tools/ab.py on variant libraries build/variants/{A,B}.so, both orders
 #                  (ARGS: extra ab.py arguments, commas for spaces)
 #   abrelay:A:B    tools/ab_relay_layout.py on the two variants (relay stream layouts)
+#   abenv:NAME=V[+NAME=V]:ARGS  tools/ab.py: the product library vs itself with those context env settings
 set -u
 OUT=${1:?usage: tools/gpu.sh OUT STEP...}
 shift
@@ -60,6 +61,13 @@ for step in "$@"; do
         grep '^{' "$O/bench_batcher_one.txt" >> "$O/bench_batcher.jsonl"
       done ;;
     hostlink) run hostlink 240 build/hostlink ;;
+    bbprof:*)  # rocprofv3 kernel stats of one bench_batcher run (ARGS comma-separated)
+      A=${step#bbprof:}
+      T=bbprof_$(echo "$A" | tr -c 'a-z0-9' '_')
+      (cd /tmp && run $T 180 rocprofv3 --kernel-trace --stats -d "$O/$T" -o run --output-format csv \
+        -- "$R/build/bench_batcher" ${A//,/ } --threads 8 --seconds 2) || exit $?
+      # keep the per-dispatch trace small: the first 20k dispatches
+      f=$(find "$O/$T" -name '*kernel_trace.csv' | head -1); [ -n "$f" ] && head -20000 "$f" > "$O/$T/trace_head.csv" && rm -f "$f" ;;
     bb:*)  # one bench_batcher run, arguments comma-separated: bb:--op,seal,--window,16384
       A=${step#bb:}
       CYAES_BATCHER_PROFILE=1 run bench_batcher_one 120 build/bench_batcher ${A//,/ } --threads ${BB_THREADS:-8} --seconds ${BB_SECONDS:-4}
@@ -70,6 +78,13 @@ for step in "$@"; do
       RL="build/variants/$B.so build/variants/$A.so"
       run ab_${A}_vs_${B} 300 python tools/ab.py $L ${ARGS//,/ }
       run ab_${B}_vs_${A} 300 python tools/ab.py $RL ${ARGS//,/ } ;;
+    abenv:*)  # abenv:NAME=V[+NAME=V]:ARGS -- the product library against itself with those context settings
+      IFS=: read -r _ ENVS ARGS <<< "$step"
+      L="cyclone_amd/libcyaes.so cyclone_amd/libcyaes.so:${ENVS//+/:}"
+      RL="cyclone_amd/libcyaes.so:${ENVS//+/:} cyclone_amd/libcyaes.so"
+      T=abenv_$(echo "$ENVS$ARGS" | tr -c 'A-Za-z0-9' '_')
+      run ${T} 300 python tools/ab.py $L ${ARGS//,/ }
+      run ${T}_rev 300 python tools/ab.py $RL ${ARGS//,/ } ;;
     abrelay:*)
       IFS=: read -r _ A B <<< "$step"
       run abrelay_${A}_vs_${B} 300 python tools/ab_relay_layout.py --lib build/variants/$A.so build/variants/$B.so ;;
