@@ -143,15 +143,16 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     // as one block stream (contiguous, so the chunk prefetch never stops at a
     // payload start), with R payloads per lane-chain still leaving >= one work
     // item per lane; sessions must hold whole runs.
+    const bool runs_ok = !offsets && !iv_in && !iv_out && !key_idx && payload_bytes <= kRunMaxPayload;
     uint64_t R = 1;
-    if (!offsets && !iv_in && !iv_out && !key_idx && payload_bytes <= kRunMaxPayload) {
+    if (runs_ok) {
         const uint64_t lanes = (uint64_t)std::max(1, ctx->num_cus) * kEncThreads;
-        R = std::min<uint64_t>(kRunMax, npayloads / lanes);
+        R = std::max<uint64_t>(1, std::min<uint64_t>(kRunMax, npayloads / lanes));
         while (R > 1 && ppk % R) R--;
     }
     if (ctx->enc_run) R = ctx->enc_run;  // A/B override (env CYAES_ENC_RUN)
-    if (offsets || iv_in || iv_out || key_idx || (ppk && ppk % R)) R = 1;
-    a.run = (uint32_t)std::max<uint64_t>(1, R);
+    if (!runs_ok || R == 0 || (ppk && ppk % R)) R = 1;
+    a.run = (uint32_t)R;
     const Shape sh = wave_shape(ctx, ((npayloads + a.run - 1) / a.run + 63) / 64, kEncThreads);
     return map_err(launch_encrypt(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
 }
