@@ -484,7 +484,9 @@ void cyaes_batcher::build_loop() {
                     return stop || flushers.load() > 0 || queued_bytes.load() >= (int64_t)cfg.max_batch_bytes;
                 });
             }
-            if (free_stages.empty() && pending) {  // every stage in flight: the pending one must drain
+            // Every other stage in flight has been handed to the completion
+            // thread and will come back; only a lone pending stage must drain.
+            if (free_stages.empty() && pending && stages.size() == 1) {
                 lk.unlock();
                 flush_pending();
                 lk.lock();
