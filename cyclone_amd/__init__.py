@@ -114,6 +114,7 @@ _SIGS = {
     "cyaes_batcher_register_pool": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _u32p]),
     "cyaes_batcher_unregister_pool": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     "cyaes_batcher_submit_pooled": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
+    "cyaes_batcher_poll": (ctypes.c_uint32, [_vp, _vp, _vp, ctypes.c_uint32]),
     "cyaes_batcher_stats": (ctypes.c_int, [_vp, _u64p]),
 }
 
@@ -435,7 +436,10 @@ class PoolReq(ctypes.Structure):
 class BatcherConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("max_batch_bytes", ctypes.c_uint32),
                 ("max_delay_us", ctypes.c_uint32), ("inflight", ctypes.c_uint32), ("workers", ctypes.c_uint32),
-                ("max_sessions", ctypes.c_uint32)]
+                ("max_sessions", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+BATCHER_POLL = 1
 
 
 class Batcher:
@@ -445,9 +449,15 @@ class Batcher:
     alive by the batcher until the request completes.  `done(status)` runs on
     the batcher's completion thread."""
 
-    def __init__(self, device=0, max_batch_bytes=0, max_delay_us=0, inflight=0, workers=0, max_sessions=0, lib=None):
+    def __init__(self, device=0, max_batch_bytes=0, max_delay_us=0, inflight=0, workers=0, max_sessions=0,
+                 poll=False, lib=None):
+        """poll=True: CYAES_BATCHER_POLL -- requests complete into the submitting
+        thread's queue (read with poll()); their `done` value is returned there
+        as a tag instead of being called."""
         self._lib = lib if lib is not None else load_library()
-        cfg = BatcherConfig(device, max_batch_bytes, max_delay_us, inflight, workers, max_sessions)
+        self._poll = bool(poll)
+        cfg = BatcherConfig(device, max_batch_bytes, max_delay_us, inflight, workers, max_sessions,
+                            BATCHER_POLL if poll else 0)
         h = _vp()
         _check(self._lib.cyaes_batcher_create(ctypes.byref(cfg), ctypes.byref(h)), "cyaes_batcher_create")
         self._h = h
@@ -472,6 +482,21 @@ class Batcher:
             bufs, done = self._live.pop(user)
         if done is not None:
             done(status)
+
+    def _cbp(self):
+        return _DONE_FN() if self._poll else self._cb  # (a NULL function pointer in poll mode)
+
+    def poll(self, max_n=65536):
+        """Poll mode: [(tag, status)] of this thread's completed requests, oldest first."""
+        users = (_vp * max_n)()
+        sts = (ctypes.c_int * max_n)()
+        n = self._lib.cyaes_batcher_poll(self._h, users, sts, max_n)
+        out = []
+        with self._mu:
+            for i in range(n):
+                _, tag = self._live.pop(users[i])
+                out.append((tag, int(sts[i])))
+        return out
 
     def _track(self, bufs, done):
         with self._mu:
@@ -503,7 +528,7 @@ class Batcher:
         if size > src.n or size > dst.n:
             raise ValueError("size exceeds buffer")
         token = self._track((src, dst), done)
-        st = self._lib.cyaes_batcher_submit(self._h, op, slot, src.ptr, dst.ptr, size, self._cb, token)
+        st = self._lib.cyaes_batcher_submit(self._h, op, slot, src.ptr, dst.ptr, size, self._cbp(), token)
         if st:
             self._untrack(token)
             raise CyaesError(st, "submit")
@@ -514,7 +539,7 @@ class Batcher:
         if dst.n < relay_packet_bytes(src.n):
             raise ValueError("packet_out too small")
         token = self._track((src, dst), done)
-        st = self._lib.cyaes_batcher_submit_seal(self._h, slot, conn_id, src.ptr, src.n, dst.ptr, self._cb, token)
+        st = self._lib.cyaes_batcher_submit_seal(self._h, slot, conn_id, src.ptr, src.n, dst.ptr, self._cbp(), token)
         if st:
             self._untrack(token)
             raise CyaesError(st, "submit_seal")
@@ -522,7 +547,7 @@ class Batcher:
     def submit_open(self, slot, packet, done=None):
         buf = _Buf(packet, True)
         token = self._track((buf,), done)
-        st = self._lib.cyaes_batcher_submit_open(self._h, slot, buf.ptr, buf.n, self._cb, token)
+        st = self._lib.cyaes_batcher_submit_open(self._h, slot, buf.ptr, buf.n, self._cbp(), token)
         if st:
             self._untrack(token)
             raise CyaesError(st, "submit_open")
@@ -553,7 +578,7 @@ class Batcher:
                 raise ValueError("request %d: size exceeds its buffer" % i)
             token = self._track((src, dst), done)
             tokens.append(token)
-            arr[i] = BatchReq(op, slot, conn or 0, src.ptr, dst.ptr, size, self._cb, token)
+            arr[i] = BatchReq(op, slot, conn or 0, src.ptr, dst.ptr, size, self._cbp(), token)
         st = (ctypes.c_int * max(1, n))()
         self._lib.cyaes_batcher_submit_many(self._h, arr, n, st)
         for i, token in enumerate(tokens):
@@ -585,7 +610,7 @@ class Batcher:
         for i, (op, slot, pool, in_off, out_off, size, done, conn) in enumerate(reqs):
             token = self._track((), done)
             tokens.append(token)
-            arr[i] = PoolReq(op, slot, conn or 0, pool, in_off, out_off or 0, size, self._cb, token)
+            arr[i] = PoolReq(op, slot, conn or 0, pool, in_off, out_off or 0, size, self._cbp(), token)
         st = (ctypes.c_int * max(1, n))()
         self._lib.cyaes_batcher_submit_pooled(self._h, arr, n, st)
         for i, token in enumerate(tokens):

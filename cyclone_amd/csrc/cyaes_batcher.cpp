@@ -172,11 +172,17 @@ class Pool {
     bool stop_ = false;
 };
 
+struct Done {
+    void* user;
+    int status;
+};
 struct alignas(64) Shard {
     std::mutex mu;
     std::vector<Pend> q;
     uint64_t bytes = 0;     // stage bytes queued in q
     uint64_t enqueued = 0;  // requests ever enqueued here (flush targets, key-row stamps, stats)
+    alignas(64) std::mutex cmu;  // CYAES_BATCHER_POLL completion queue
+    std::deque<Done> cq;
 };
 int my_shard() {
     static std::atomic<int> next{0};
@@ -683,8 +689,25 @@ void cyaes_batcher::complete_loop() {
         const int64_t t2 = now_ns();
         pc.copy_out += t2 - t1;
         // Callbacks: one job per shard run, in that shard's submission order.
-        workers->run(st->segs.size(), [st, status](size_t k) {
+        // Poll mode: requests without a callback go to their shard's queue in
+        // one locked append per run.
+        const bool poll = (cfg.flags & CYAES_BATCHER_POLL) != 0;
+        workers->run(st->segs.size(), [this, st, status, poll](size_t k) {
             const Seg& g = st->segs[k];
+            if (poll) {
+                thread_local std::vector<Done> out;
+                out.clear();
+                for (uint32_t i = g.begin; i < g.end; i++) {
+                    if (st->cbs[i].done) st->cbs[i].done(st->cbs[i].user, status);
+                    else out.push_back({st->cbs[i].user, status});
+                }
+                if (!out.empty()) {
+                    Shard& sh = shards[g.shard];
+                    std::lock_guard<std::mutex> lk(sh.cmu);
+                    sh.cq.insert(sh.cq.end(), out.begin(), out.end());
+                }
+                return;
+            }
             for (uint32_t i = g.begin; i < g.end; i++)
                 if (st->cbs[i].done) st->cbs[i].done(st->cbs[i].user, status);
         });
@@ -745,7 +768,7 @@ int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out) {
     if (c.workers == 0) c.workers = 4;
     if (c.max_sessions == 0) c.max_sessions = 65536;
     if (c.max_batch_bytes < 4096 || c.max_batch_bytes > (1u << 30) || c.inflight > 16 || c.workers > 64 ||
-        c.max_sessions > (1u << 22))
+        c.max_sessions > (1u << 22) || (c.flags & ~CYAES_BATCHER_POLL))
         return CYAES_EINVAL;
     cyaes_gpu* ctx = nullptr;
     int st = cyaes_gpu_create(c.device, &ctx);
@@ -1049,6 +1072,19 @@ int cyaes_batcher_submit_open(cyaes_batcher* b, uint32_t slot, uint8_t* packet, 
     int st = CYAES_OK;
     const int rc = cyaes_batcher_submit_many(b, &q, 1, &st);
     return rc ? rc : st;
+}
+
+uint32_t cyaes_batcher_poll(cyaes_batcher* b, void** users, int* status, uint32_t max) {
+    if (!b || !users || max == 0) return 0;
+    Shard& sh = b->shards[my_shard()];
+    std::lock_guard<std::mutex> lk(sh.cmu);
+    const uint32_t n = (uint32_t)std::min<size_t>(max, sh.cq.size());
+    for (uint32_t i = 0; i < n; i++) {
+        users[i] = sh.cq[i].user;
+        if (status) status[i] = sh.cq[i].status;
+    }
+    sh.cq.erase(sh.cq.begin(), sh.cq.begin() + n);
+    return n;
 }
 
 int cyaes_batcher_flush(cyaes_batcher* b) {

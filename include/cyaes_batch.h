@@ -70,7 +70,16 @@ typedef struct cyaes_batcher_config {
     uint32_t inflight;        /* stages / batches in flight (0 => 3)                   */
     uint32_t workers;         /* completion-side threads: callbacks, bounce copies (0 => 4) */
     uint32_t max_sessions;    /* device key-table rows (0 => 65536)                    */
+    uint32_t flags;           /* CYAES_BATCHER_POLL                                    */
 } cyaes_batcher_config;
+
+/* Completion queues instead of callbacks: with this flag a request submitted
+ * with done == NULL completes into its submitting thread's queue, which the
+ * thread drains with cyaes_batcher_poll -- the way a relay looper picks up its
+ * finished packets on its own thread before TcpConnection::send
+ * (relay_local.cpp:206-216), one lock per batch instead of one call per
+ * packet.  (Without the flag, done == NULL means no notification.) */
+#define CYAES_BATCHER_POLL 1u
 
 int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out);
 /* Completes every submitted request, then frees everything. */
@@ -140,6 +149,12 @@ typedef struct cyaes_pool_req {
     void* user;
 } cyaes_pool_req;
 int cyaes_batcher_submit_pooled(cyaes_batcher* b, const cyaes_pool_req* reqs, uint32_t n, int* status);
+
+/* CYAES_BATCHER_POLL: pops up to max completions (user pointer, status) of
+ * the calling thread's queue, oldest first (a thread's requests complete in
+ * its submission order; threads that share a submission shard share a queue).
+ * Returns the number popped; never blocks. */
+uint32_t cyaes_batcher_poll(cyaes_batcher* b, void** users, int* status, uint32_t max);
 
 /* Blocks until every request submitted before the call has completed
  * (callbacks returned).  Returns the first error status seen since the

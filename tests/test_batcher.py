@@ -572,3 +572,50 @@ def test_bench_batcher_output_matches_relay_oracle(tmp_path, op, extra):
                 assert out == ro.open_forward(key, inp)[2]
             nchecked += 1
     assert nchecked == 3 * 64
+
+
+def test_poll_mode_completions_in_submission_order():
+    """CYAES_BATCHER_POLL: requests complete into the submitting thread's queue
+    (cyaes_batcher_poll) in its submission order, instead of one callback per
+    packet; SEAL and OPEN on pool memory against the relay restatement."""
+    import numpy as np
+    b = ca.Batcher(0, max_batch_bytes=1 << 20, max_delay_us=100, poll=True)
+    try:
+        key = _keys(1, 41)[0]
+        slot = b.session_open(key)
+        rng = random.Random(41)
+        pool = np.zeros(16 << 20, dtype=np.uint8)
+        pid = b.register_pool(pool)
+        reqs, want, off = [], [], 0
+        for i in range(3000):
+            n = rng.choice([0, 16, 100, 1472, 5000])
+            chunk = bytes(rng.getrandbits(8) for _ in range(n))
+            pool[off:off + n] = np.frombuffer(chunk, np.uint8)
+            out = off + ((n + 63) // 64) * 64
+            reqs.append((ca.OP_RELAY_SEAL, slot, pid, off, out, n, i, 9))
+            want.append((out, ro.seal_forward(key, 9, chunk)))
+            off = out + ((ca.relay_packet_bytes(n) + 63) // 64) * 64
+        assert b.submit_pooled(reqs) == [0] * len(reqs)
+        got = []
+        import time
+        t_end = time.time() + 60
+        while len(got) < len(reqs) and time.time() < t_end:
+            got += b.poll()
+            if len(got) < len(reqs):
+                time.sleep(0.001)
+        assert [t for t, _ in got] == list(range(len(reqs)))  # submission order
+        assert all(st == ca.CYAES_OK for _, st in got)
+        for o, w in want:
+            assert bytes(pool[o:o + len(w)]) == w
+        # OPEN the sealed packets in place, polled again
+        opens = [(ca.OP_RELAY_OPEN, slot, pid, o, 0, len(w), ("open", k), 0) for k, (o, w) in enumerate(want)]
+        assert b.submit_pooled(opens) == [0] * len(opens)
+        assert b.flush() == ca.CYAES_OK  # (flush covers poll-mode requests too)
+        got = b.poll()
+        assert [t for t, _ in got] == [("open", k) for k in range(len(want))]
+        for o, w in want:
+            assert bytes(pool[o:o + len(w)]) == ro.open_forward(key, w)[2]
+        assert b.poll() == []
+        b.unregister_pool(pid)
+    finally:
+        b.close()

@@ -24,6 +24,10 @@
 //                      [--window W] [--seconds S] [--batch-mb M] [--delay-us D]
 //                      [--workers K] [--inflight I] [--bulk 0|1] [--pool 0|1]
 //                      [--submit ptr|pooled] [--reopen-copy 0|1] [--dump FILE]
+//                      [--complete callback|poll]
+// --complete poll: the batcher runs with CYAES_BATCHER_POLL and each looper
+// drains its own completion queue (cyaes_batcher_poll) in its loop instead of
+// receiving one callback per packet.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -57,7 +61,7 @@ struct Looper {
     uint32_t size = 1472;
     uint8_t* mem = nullptr;  // the slots' buffers
     uint32_t pool = ~0u;     // registered pool id (~0u: not registered)
-    bool pooled_submit = false, reopen_copy = false;
+    bool pooled_submit = false, reopen_copy = false, poll = false;
     std::vector<Slot> slots;
     std::mutex mu;
     std::vector<Slot*> ready;  // completed, to resubmit
@@ -92,27 +96,29 @@ static int submit(Looper* L, Slot* s) {
 
 static cyaes_batch_req make_req(Looper* L, Slot* s) {
     s->t0 = Clock::now();
+    cyaes_done_fn cb = L->poll ? nullptr : on_done;
     switch (L->op) {
         case CYAES_OP_RELAY_SEAL:
-            return {CYAES_OP_RELAY_SEAL, L->session, 7, s->in, s->out, L->size, on_done, s};
+            return {CYAES_OP_RELAY_SEAL, L->session, 7, s->in, s->out, L->size, cb, s};
         case CYAES_OP_RELAY_OPEN:
             if (L->reopen_copy) memcpy(s->out, s->in, s->in_n);
-            return {CYAES_OP_RELAY_OPEN, L->session, 0, nullptr, s->out, s->out_n, on_done, s};
+            return {CYAES_OP_RELAY_OPEN, L->session, 0, nullptr, s->out, s->out_n, cb, s};
         default:
-            return {L->op, L->session, 0, s->in, s->out, L->size, on_done, s};
+            return {L->op, L->session, 0, s->in, s->out, L->size, cb, s};
     }
 }
 
 static cyaes_pool_req make_pool_req(Looper* L, Slot* s) {
     s->t0 = Clock::now();
+    cyaes_done_fn cb = L->poll ? nullptr : on_done;
     switch (L->op) {
         case CYAES_OP_RELAY_SEAL:
-            return {CYAES_OP_RELAY_SEAL, L->session, 7, L->pool, s->in_off, s->out_off, L->size, on_done, s};
+            return {CYAES_OP_RELAY_SEAL, L->session, 7, L->pool, s->in_off, s->out_off, L->size, cb, s};
         case CYAES_OP_RELAY_OPEN:
             if (L->reopen_copy) memcpy(s->out, s->in, s->in_n);
-            return {CYAES_OP_RELAY_OPEN, L->session, 0, L->pool, s->out_off, 0, s->out_n, on_done, s};
+            return {CYAES_OP_RELAY_OPEN, L->session, 0, L->pool, s->out_off, 0, s->out_n, cb, s};
         default:
-            return {L->op, L->session, 0, L->pool, s->in_off, s->out_off, L->size, on_done, s};
+            return {L->op, L->session, 0, L->pool, s->in_off, s->out_off, L->size, cb, s};
     }
 }
 
@@ -127,7 +133,7 @@ int main(int argc, char** argv) {
     std::string op = "seal";
     uint32_t size = 1472, threads = 8, window = 512, batch_mb = 32, delay_us = 100, workers = 8, inflight = 3, bulk = 1;
     uint32_t use_pool = 1, reopen_copy = 0;
-    std::string submit_kind = "ptr", dump;
+    std::string submit_kind = "ptr", dump, complete = "callback";
     double seconds = 5;
     for (int i = 1; i + 1 < argc; i += 2) {
         std::string a = argv[i];
@@ -145,7 +151,9 @@ int main(int argc, char** argv) {
         else if (a == "--submit") submit_kind = argv[i + 1];
         else if (a == "--reopen-copy") reopen_copy = atoi(argv[i + 1]);
         else if (a == "--dump") dump = argv[i + 1];
+        else if (a == "--complete") complete = argv[i + 1];
     }
+    const bool poll = complete == "poll";
     const bool pooled_submit = submit_kind == "pooled";
     if (pooled_submit && !use_pool) {
         fprintf(stderr, "--submit pooled needs --pool 1\n");
@@ -156,7 +164,7 @@ int main(int argc, char** argv) {
     if ((opc == CYAES_OP_ENCRYPT || opc == CYAES_OP_DECRYPT) && size % 16) size = cyaes_relay_round16(size);
     if (opc >= CYAES_OP_RELAY_SEAL && size > CYAES_RELAY_MAX_CHUNK) size = CYAES_RELAY_MAX_CHUNK;
 
-    cyaes_batcher_config cfg = {0, batch_mb << 20, delay_us, inflight, workers, 0};
+    cyaes_batcher_config cfg = {0, batch_mb << 20, delay_us, inflight, workers, 0, poll ? CYAES_BATCHER_POLL : 0u};
     cyaes_batcher* b = nullptr;
     int st = cyaes_batcher_create(&cfg, &b);
     if (st) {
@@ -175,6 +183,7 @@ int main(int argc, char** argv) {
         L.size = size;
         L.pooled_submit = pooled_submit;
         L.reopen_copy = reopen_copy != 0;
+        L.poll = false;  // the warm-up and --dump rounds use callbacks (the loopers switch below)
         uint8_t key[16];
         for (int i = 0; i < 16; i++) key[i] = (uint8_t)(t * 16 + i);
         cyaes_batcher_session_open(b, key, &L.session);
@@ -243,13 +252,34 @@ int main(int argc, char** argv) {
     const auto t0 = Clock::now();
     std::vector<std::thread> th;
     for (auto& L : loopers) {
+        L.poll = poll;
         th.emplace_back([&L, &stop, bulk] {
-            for (auto& s : L.slots) submit(&L, &s);
+            for (auto& s : L.slots) {
+                if (L.poll) {  // (this thread's first submits: its completions come to its own queue)
+                    cyaes_batch_req q = make_req(&L, &s);
+                    cyaes_batcher_submit_many(L.b, &q, 1, nullptr);
+                } else {
+                    submit(&L, &s);
+                }
+            }
             std::vector<Slot*> again;
             std::vector<cyaes_batch_req> reqs;
             std::vector<cyaes_pool_req> preqs;
+            std::vector<void*> users(L.slots.size());
+            std::vector<int> sts(L.slots.size());
             while (!stop.load(std::memory_order_relaxed)) {
-                {
+                if (L.poll) {  // drain this thread's completion queue
+                    const uint32_t n = cyaes_batcher_poll(L.b, users.data(), sts.data(), (uint32_t)users.size());
+                    const auto now = Clock::now();
+                    for (uint32_t i = 0; i < n; i++) {
+                        Slot* s = static_cast<Slot*>(users[i]);
+                        if (sts[i]) L.err = sts[i];
+                        if (L.lat_us.size() < 2000000)
+                            L.lat_us.push_back(std::chrono::duration<double, std::micro>(now - s->t0).count());
+                        again.push_back(s);
+                    }
+                    L.done.fetch_add(n, std::memory_order_relaxed);
+                } else {
                     std::lock_guard<std::mutex> lk(L.mu);
                     again.swap(L.ready);
                 }
@@ -261,7 +291,7 @@ int main(int argc, char** argv) {
                     preqs.clear();
                     for (Slot* s : again) preqs.push_back(make_pool_req(&L, s));
                     cyaes_batcher_submit_pooled(L.b, preqs.data(), (uint32_t)preqs.size(), nullptr);
-                } else if (bulk) {  // one cyaes_batcher_submit_many per poll, as a relay looper would
+                } else if (bulk || L.poll) {  // one cyaes_batcher_submit_many per poll, as a relay looper would
                     reqs.clear();
                     for (Slot* s : again) reqs.push_back(make_req(&L, s));
                     cyaes_batcher_submit_many(L.b, reqs.data(), (uint32_t)reqs.size(), nullptr);
@@ -312,12 +342,12 @@ int main(int argc, char** argv) {
 
     printf("{\"metric\": \"batcher %s requests/s host-to-host\", \"op\": \"%s\", \"size\": %u, \"threads\": %u, "
            "\"window\": %u, \"batch_mb\": %u, \"delay_us\": %u, \"workers\": %u, \"inflight\": %u, \"bulk\": %u, "
-           "\"pool\": %u, \"submit\": \"%s\", \"seconds\": %.2f, \"requests\": %llu, "
+           "\"pool\": %u, \"submit\": \"%s\", \"complete\": \"%s\", \"seconds\": %.2f, \"requests\": %llu, "
            "\"requests_per_s\": %.0f, \"payload_gibs\": %.3f, \"mean_batch\": %.1f, \"lat_p50_us\": %.0f, "
            "\"lat_p99_us\": %.0f, \"errors\": %d, \"sync_dropin_calls_per_s\": %.0f, "
            "\"sync_dropin_gibs\": %.4f}\n",
            op.c_str(), op.c_str(), size, threads, window, batch_mb, delay_us, workers, inflight, bulk, use_pool,
-           submit_kind.c_str(), el, (unsigned long long)counted,
+           submit_kind.c_str(), complete.c_str(), el, (unsigned long long)counted,
            counted / el, counted * payload / el / (1u << 30), batches > 0 ? (st1[0] - st0[0]) / batches : 0.0, p50,
            p99, err, calls / sync_s, calls * (double)buf.size() / sync_s / (1u << 30));
     return err ? 2 : 0;
