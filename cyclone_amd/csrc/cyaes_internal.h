@@ -88,6 +88,7 @@ struct EncArgs {
     const uint32_t* tables;  // kEncTableWords
     uint32_t* status;
     uint32_t run;            // uniform lane kernel: payloads per work item (> 1: k_encrypt RUNS; no IV arrays)
+    uint32_t sess_payloads;  // uniform lane kernel: payloads_per_key when every wave lies in one session (SESS), else 0
 };
 
 struct DecArgs {

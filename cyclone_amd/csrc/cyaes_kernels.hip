@@ -406,7 +406,11 @@ __device__ __forceinline__ void drain_loads() { asm volatile("s_waitcnt vmcnt(0)
 // config B (1,472-B payloads) streams 368 blocks instead of four 92-block
 // payloads, each of which started on an exposed load and ended in a 4-block
 // tail.  The restart test is on wave-uniform block counters (scalar).
-template <bool RAGGED, bool KEYED, bool RUNS>
+// SESS (uniform batches keyed by sessions of payloads_per_key payloads that
+// are whole waves long, config D): a wave's work items all lie in one session,
+// so its key comes from the scalar position, per wave, in SGPRs -- the
+// unkeyed code path, no per-lane key index and no waterfall.
+template <bool RAGGED, bool KEYED, bool RUNS, bool SESS>
 __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
     fill_region(lds_words, a.tables, a.tables + 512, blockDim.x);              // TL1 | TL3
@@ -428,7 +432,8 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     const uint32_t bpp = a.payload_bytes >> 4;
     const uint64_t nwork = RUNS ? (a.npayloads + R - 1) / R : a.npayloads;
     uint32_t ek[44];
-    if (!KEYED) load_sched(a.keys, 0, 0, ek);  // one schedule for the whole batch
+    uint32_t ek_sess = 0;  // SESS: the session whose schedule ek holds
+    if (!KEYED) load_sched(a.keys, 0, 0, ek);  // one schedule for the whole batch (SESS: session 0's)
 
     for (uint64_t wbase = wbase0; wbase < nwork; wbase += wstride) {
         const uint64_t w = wbase + lane;
@@ -445,6 +450,13 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
         }
         // RUNS + KEYED: the runtime makes runs divide payloads_per_key, so the run is one session
         const uint32_t kid = KEYED ? key_index(a.keys, p, a.npayloads, active, a.status) : 0u;
+        if (SESS) {  // the wave's session, from its first work item (scalar)
+            const uint32_t ks = (uint32_t)(__builtin_amdgcn_readfirstlane((uint32_t)(wbase * R / a.sess_payloads)));
+            if (ks != ek_sess) {
+                load_sched(a.keys, ks, 0, ek);
+                ek_sess = ks;
+            }
+        }
         bool pending = active;
         while (true) {  // waterfall over the distinct keys of this wave
             const uint64_t m = __ballot(pending);
@@ -1218,12 +1230,15 @@ hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t s
     const bool ragged = a.offsets != nullptr;
     const dim3 g(grid), b(threads);
     const bool runs = !ragged && a.run > 1;
-    if (ragged && keyed) hipLaunchKernelGGL((k_encrypt<true, true, false>), g, b, 0, stream, a);
-    else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false, false>), g, b, 0, stream, a);
-    else if (runs && keyed) hipLaunchKernelGGL((k_encrypt<false, true, true>), g, b, 0, stream, a);
-    else if (runs) hipLaunchKernelGGL((k_encrypt<false, false, true>), g, b, 0, stream, a);
-    else if (keyed) hipLaunchKernelGGL((k_encrypt<false, true, false>), g, b, 0, stream, a);
-    else hipLaunchKernelGGL((k_encrypt<false, false, false>), g, b, 0, stream, a);
+    const bool sess = !ragged && a.sess_payloads != 0;  // keyed by whole-wave sessions: the unkeyed body per session
+    if (ragged && keyed) hipLaunchKernelGGL((k_encrypt<true, true, false, false>), g, b, 0, stream, a);
+    else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false, false, false>), g, b, 0, stream, a);
+    else if (sess && runs) hipLaunchKernelGGL((k_encrypt<false, false, true, true>), g, b, 0, stream, a);
+    else if (sess) hipLaunchKernelGGL((k_encrypt<false, false, false, true>), g, b, 0, stream, a);
+    else if (runs && keyed) hipLaunchKernelGGL((k_encrypt<false, true, true, false>), g, b, 0, stream, a);
+    else if (runs) hipLaunchKernelGGL((k_encrypt<false, false, true, false>), g, b, 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_encrypt<false, true, false, false>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((k_encrypt<false, false, false, false>), g, b, 0, stream, a);
     return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@ struct cyaes_gpu {
     uint64_t quad_max_chains = CYAES_QUAD_MAX_CHAINS;  // env CYAES_QUAD_MAX_CHAINS (A/B only)
     uint32_t ragged_group = 0;  // env CYAES_RAGGED_GROUP: payloads per ragged-decrypt wave group (0 = auto; tests, A/B)
     uint32_t enc_run = 0;       // env CYAES_ENC_RUN: payloads per lane run of the uniform encrypt (0 = auto; tests, A/B)
+    bool enc_no_sess = false;   // env CYAES_ENC_NO_SESS=1: keyed uniform encrypt always by waterfall (tests, A/B)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
     uint32_t* d_keys = nullptr;    // nkeys * kSchedWords
     uint32_t nkeys = 0;
@@ -143,10 +144,11 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     // as one block stream (contiguous, so the chunk prefetch never stops at a
     // payload start), with R payloads per lane-chain still leaving >= one work
     // item per lane; sessions must hold whole runs.
-    // (Unkeyed only: with per-session keys (config D) runs measured 3 % slower,
-    // without them (config B) 1.5 % faster, profiles/r03/ab_enc_runs.txt.)
+    // (With per-session keys on the waterfall path (config D) runs measured 3 %
+    // slower, without keys (config B) 1.5 % faster, profiles/r03/ab_enc_runs.txt;
+    // whole-wave sessions take the SESS path below, which has no waterfall.)
     const bool runs_ok = !offsets && !iv_in && !iv_out && !key_idx && payload_bytes <= kRunMaxPayload;
-    const bool runs_auto = runs_ok && !ppk;
+    const bool runs_auto = runs_ok;
     uint64_t R = 1;
     if (runs_auto) {
         const uint64_t lanes = (uint64_t)std::max(1, ctx->num_cus) * kEncThreads;
@@ -155,7 +157,22 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     }
     if (ctx->enc_run) R = ctx->enc_run;  // A/B override (env CYAES_ENC_RUN)
     if (!runs_ok || R == 0 || (ppk && ppk % R)) R = 1;
+    // Sessions of payloads_per_key payloads that hold whole waves of work items
+    // (64 lanes x R payloads; config D: 256 = 64 x 4): the key is per wave
+    // (SESS).  Otherwise keyed batches take the per-lane waterfall, without runs
+    // unless forced.
+    bool sess = false;
+    if (!offsets && !key_idx && ppk && !ctx->enc_no_sess) {
+        uint64_t r = R;
+        while (r > 1 && ppk % (64 * r)) r--;
+        if (ppk % (64 * r) == 0) {
+            sess = true;
+            R = r;
+        }
+    }
+    if (ppk && !sess && !ctx->enc_run) R = 1;
     a.run = (uint32_t)R;
+    a.sess_payloads = sess ? ppk : 0;
     const Shape sh = wave_shape(ctx, ((npayloads + a.run - 1) / a.run + 63) / 64, kEncThreads);
     return map_err(launch_encrypt(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
 }
@@ -340,6 +357,7 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* q = getenv("CYAES_QUAD_MAX_CHAINS")) ctx->quad_max_chains = strtoull(q, nullptr, 10);
     if (const char* g = getenv("CYAES_RAGGED_GROUP")) ctx->ragged_group = (uint32_t)strtoul(g, nullptr, 10);
     if (const char* r = getenv("CYAES_ENC_RUN")) ctx->enc_run = (uint32_t)strtoul(r, nullptr, 10);
+    if (const char* v = getenv("CYAES_ENC_NO_SESS")) ctx->enc_no_sess = atoi(v) != 0;
     const HostTables& t = host_tables();
     uint8_t host[kTablesBytes];
     memcpy(host + kEncTableOff, t.enc, sizeof(t.enc));

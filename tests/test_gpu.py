@@ -633,3 +633,32 @@ def test_full_config_digest(torch, golden, name):
     del d_pt, d_ct
     torch.cuda.empty_cache()
     c.close()
+
+
+@pytest.mark.parametrize("run,pb,ppk,nk", [("1", 1472, 64, 9), ("2", 1472, 256, 5), ("4", 208, 256, 7),
+                                           ("2", 1472, 192, 6), ("0", 1024, 128, 20)])
+def test_encrypt_whole_wave_sessions_and_runs(torch, run, pb, ppk, nk):
+    """k_encrypt SESS (sessions that hold whole waves of work items: the key
+    is per wave, from the scalar position) with and without RUNS (R
+    consecutive payloads per lane as one block stream, chain restarts at
+    DefaultIV), forced onto small batches through the lane kernel, against the
+    oracle; the last session and the last run are partial."""
+    n = ppk * nk - 37
+    keys = [oracle.session_key(s) for s in range(nk)]
+    old = {k: os.environ.get(k) for k in ("CYAES_QUAD_MAX_CHAINS", "CYAES_ENC_RUN")}
+    os.environ["CYAES_QUAD_MAX_CHAINS"] = "0"
+    os.environ["CYAES_ENC_RUN"] = run
+    try:
+        c = ca.GpuContext(0)
+    finally:
+        _restore(old)
+    c.set_keys(b"".join(keys))
+    pt = oracle.synthetic(5, n, pb)
+    want = oracle.batch(False, keys, ppk, pt, pb, nthreads=16)
+    d_pt, d_ct, d_rt = dev(torch, pt), empty(torch, pt.size), empty(torch, pt.size)
+    c.encrypt_uniform(d_pt, d_ct, n, pb, payloads_per_key=ppk)
+    c.decrypt_uniform(d_ct, d_rt, n, pb, payloads_per_key=ppk)
+    assert np.array_equal(host(d_ct), want)
+    assert np.array_equal(host(d_rt), pt)
+    assert c.check() == ca.CYAES_OK
+    c.close()
