@@ -782,10 +782,8 @@ int dropin_batch(cyaes_gpu* ctx, DropInSlot& d, const std::vector<DropInCall*>& 
     return CYAES_OK;
 }
 
-int dropin_run(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* out, size_t size, uint8_t* iv) {
-    if (!key || !in || !out || size % 16) return CYAES_EINVAL;
-    if (size == 0) return CYAES_OK;  // no-op, IV unchanged (cyr_rijndael.cpp:600 loop never runs)
-    if (size > 0xFFFFFFF0ull) return CYAES_EINVAL;
+// One combined call of at most dropin_piece() bytes.
+int dropin_one(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* out, size_t size, uint8_t* iv) {
     DropIn& d = dropin();
     DropInCall me{decrypt, key, in, out, (uint32_t)size, iv};
     std::unique_lock<std::mutex> lk(d.mu);
@@ -827,6 +825,39 @@ int dropin_run(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* o
         d.cv.notify_all();
     }
     return me.status;
+}
+
+// Bytes per combined call (a batch's sizes are 32-bit); env CYAES_DROPIN_PIECE
+// (a multiple of 16) lowers it so tests can reach the piece path cheaply.
+uint64_t dropin_piece() {
+    static const uint64_t piece = [] {
+        const char* e = getenv("CYAES_DROPIN_PIECE");
+        const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+        return (v >= 16 && v % 16 == 0 && v <= (1ull << 31)) ? v : (1ull << 31);
+    }();
+    return piece;
+}
+
+// Rijndael::encrypt / decrypt (cyr_rijndael.cpp:588-635).  The reference
+// asserts size % 16 == 0 and input != NULL (its typo `input && input`,
+// :590-591); size == 0 never enters its loop, whatever the pointers.  Calls
+// above dropin_piece() run as consecutive pieces of one CBC chain: the final
+// chain of a piece (for decrypt its last ciphertext block, read before an
+// in-place piece overwrites it) is the IV of the next.
+int dropin_run(bool decrypt, const cyaes_key* key, const uint8_t* in, uint8_t* out, size_t size, uint8_t* iv) {
+    if (size % 16) return CYAES_EINVAL;
+    if (size == 0) return CYAES_OK;  // no-op, IV unchanged (cyr_rijndael.cpp:600 loop never runs)
+    if (!key || !in || !out) return CYAES_EINVAL;
+    const uint64_t piece = dropin_piece();
+    if (size <= piece) return dropin_one(decrypt, key, in, out, size, iv);
+    uint8_t chain[16];
+    memcpy(chain, iv ? iv : cyaes_default_iv(), 16);
+    for (uint64_t off = 0; off < size; off += piece) {
+        const int st = dropin_one(decrypt, key, in + off, out + off, std::min<uint64_t>(piece, size - off), chain);
+        if (st) return st;
+    }
+    if (iv) memcpy(iv, chain, 16);  // cyr_rijndael.cpp:607-608, 633-634
+    return CYAES_OK;
 }
 
 }  // namespace

@@ -662,3 +662,34 @@ def test_encrypt_whole_wave_sessions_and_runs(torch, run, pb, ppk, nk):
     assert np.array_equal(host(d_rt), pt)
     assert c.check() == ca.CYAES_OK
     c.close()
+
+
+def test_dropin_size_zero_and_pieces():
+    """The drop-in's argument rules: size 0 is a no-op whatever the
+    pointers (the reference's loop never runs, cyr_rijndael.cpp:600), and a call
+    longer than one combined batch runs as consecutive pieces of one chain
+    (CYAES_DROPIN_PIECE lowers the piece size here), IV in and out, in place."""
+    import ctypes
+    lib = ca.load_library()
+    k = ca.key_expand(K0)
+    assert lib.cyaes_cbc_encrypt(ctypes.byref(k), None, None, 0, None) == ca.CYAES_OK
+    assert lib.cyaes_cbc_decrypt(ctypes.byref(k), None, None, 0, None) == ca.CYAES_OK
+    assert lib.cyaes_cbc_encrypt(ctypes.byref(k), None, None, 16, None) == ca.CYAES_EINVAL
+    code = ("import os, sys, random\n"
+            "sys.path[:0] = [%r, %r]\n"
+            "import cyclone_amd as ca, oracle\n"
+            "rng = random.Random(5)\n"
+            "for size in (4096 * 3 + 16, 4096 * 5, 16 * 1000):\n"
+            "    data = bytes(rng.getrandbits(8) for _ in range(size))\n"
+            "    iv0 = bytes(rng.getrandbits(8) for _ in range(16))\n"
+            "    a, r = ca.Rijndael(%r), oracle.Rijndael(%r)\n"
+            "    iv, riv = bytearray(iv0), bytearray(iv0)\n"
+            "    buf = bytearray(data); a.encrypt(buf, buf, size, iv)\n"
+            "    assert bytes(buf) == bytes(r.encrypt(data, None, size, riv)) and iv == riv\n"
+            "    iv, riv = bytearray(iv0), bytearray(iv0); ct = bytes(buf)\n"
+            "    a.decrypt(buf, buf, size, iv)\n"
+            "    assert bytes(buf) == data and iv == bytearray(ct[-16:])\n"
+            "print('pieces ok')\n" % (ROOT, os.path.join(ROOT, "oracle"), K0, K0))
+    env = dict(os.environ, CYAES_DROPIN_PIECE="4096")
+    r = subprocess.run([__import__("sys").executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "pieces ok" in r.stdout, r.stdout + r.stderr
