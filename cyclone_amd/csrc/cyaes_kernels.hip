@@ -409,7 +409,8 @@ __device__ __forceinline__ void drain_loads() { asm volatile("s_waitcnt vmcnt(0)
 // SESS (uniform batches keyed by sessions of payloads_per_key payloads that
 // are whole waves long, config D): a wave's work items all lie in one session,
 // so its key comes from the scalar position, per wave, in SGPRs -- the
-// unkeyed code path, no per-lane key index and no waterfall.
+// unkeyed code path, no per-lane key index and no waterfall.  The grid has a
+// lane per work item (not persistent).
 template <bool RAGGED, bool KEYED, bool RUNS, bool SESS>
 __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
@@ -432,8 +433,14 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     const uint32_t bpp = a.payload_bytes >> 4;
     const uint64_t nwork = RUNS ? (a.npayloads + R - 1) / R : a.npayloads;
     uint32_t ek[44];
-    uint32_t ek_sess = 0;  // SESS: the session whose schedule ek holds
-    if (!KEYED) load_sched(a.keys, 0, 0, ek);  // one schedule for the whole batch (SESS: session 0's)
+    // One schedule per wave, loaded before the loop: the whole batch's, or
+    // (SESS) the wave's session's, from its scalar position.  A SESS grid covers
+    // the batch in one pass (one work item per lane, the runtime sizes the
+    // grid), so the loop body runs once.  Re-loading ek inside the loop instead
+    // made the compiler schedule the round loop with 57 s_waitcnt per 160 LDS
+    // reads against 44 (config D encrypt 1.11 ms against B's 1.09).
+    if (SESS) load_sched(a.keys, wbase0 < nwork ? (uint32_t)(wbase0 * R / a.sess_payloads) : 0u, 0, ek);
+    else if (!KEYED) load_sched(a.keys, 0, 0, ek);
 
     for (uint64_t wbase = wbase0; wbase < nwork; wbase += wstride) {
         const uint64_t w = wbase + lane;
@@ -450,13 +457,6 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
         }
         // RUNS + KEYED: the runtime makes runs divide payloads_per_key, so the run is one session
         const uint32_t kid = KEYED ? key_index(a.keys, p, a.npayloads, active, a.status) : 0u;
-        if (SESS) {  // the wave's session, from its first work item (scalar)
-            const uint32_t ks = (uint32_t)(__builtin_amdgcn_readfirstlane((uint32_t)(wbase * R / a.sess_payloads)));
-            if (ks != ek_sess) {
-                load_sched(a.keys, ks, 0, ek);
-                ek_sess = ks;
-            }
-        }
         bool pending = active;
         while (true) {  // waterfall over the distinct keys of this wave
             const uint64_t m = __ballot(pending);
@@ -541,6 +541,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                 if (a.iv_out) ST16(a.iv_out + 16 * p, iv_out_e, c);  // (RUNS: no IV arrays)
             }
         }
+        if (SESS) break;  // one pass (above)
     }
 }
 

@@ -173,8 +173,13 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     if (ppk && !sess && !ctx->enc_run) R = 1;
     a.run = (uint32_t)R;
     a.sess_payloads = sess ? ppk : 0;
-    const Shape sh = wave_shape(ctx, ((npayloads + a.run - 1) / a.run + 63) / 64, kEncThreads);
-    return map_err(launch_encrypt(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
+    const uint64_t waves = ((npayloads + a.run - 1) / a.run + 63) / 64;
+    const Shape sh = wave_shape(ctx, waves, kEncThreads);
+    // SESS: one pass, a lane per work item (the kernel loads each wave's
+    // schedule once, before its loop); more workgroups than CUs queue.
+    const uint64_t sess_grid = (waves * 64 + sh.threads - 1) / sh.threads;
+    if (sess && sess_grid > (uint64_t)INT32_MAX) return CYAES_EINVAL;
+    return map_err(launch_encrypt(a, sess ? (int)sess_grid : std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
 }
 
 // Per-call device scratch, stream-ordered (hipMallocFromPoolAsync /
