@@ -23,15 +23,24 @@ PROBE    := $(BUILD)/variants/clockprobe.so
 # CYAES_LIBRARY=build/variants/bounds.so.
 BOUNDS   := $(BUILD)/variants/bounds.so
 
+# AES kernels in three translation units, each compiled with the machine
+# scheduler that measured best for its kernels (profiles/r03/ab_sched.txt):
+# the default for the quad encrypt and the ragged decrypt, iterative ILP for
+# the lane encrypt (config C -1.5 %), max ILP for the flat decrypt (-1.5 %).
 KSRC     := cyclone_amd/csrc/cyaes_kernels.hip
+ESRC     := cyclone_amd/csrc/cyaes_enc_kernels.hip
+DSRC     := cyclone_amd/csrc/cyaes_dec_kernels.hip
+SCHED_ENC:= -mllvm -amdgpu-sched-strategy=iterative-ilp
+SCHED_DEC:= -mllvm -amdgpu-sched-strategy=max-ilp
 ASRC     := cyclone_amd/csrc/cyaes_adler.hip
 BSRC     := cyclone_amd/csrc/cyaes_batch_kernels.hip
 HSRC     := cyclone_amd/csrc/cyaes_runtime.cpp cyclone_amd/csrc/cyaes_tables.cpp cyclone_amd/csrc/cyr_rijndael.cpp \
             cyclone_amd/csrc/cyaes_relay.cpp cyclone_amd/csrc/cyaes_batcher.cpp
 HDRS     := include/cyaes.h include/cyaes_relay.h include/cyaes_batch.h include/cyclone_amd/cyr_rijndael.h cyclone_amd/csrc/cyaes_internal.h \
             cyclone_amd/csrc/cyaes_tables.h
+KHDRS    := $(HDRS) cyclone_amd/csrc/cyaes_device.h
 
-KOBJ     := $(BUILD)/cyaes_kernels.o
+KOBJ     := $(BUILD)/cyaes_kernels.o $(BUILD)/cyaes_enc_kernels.o $(BUILD)/cyaes_dec_kernels.o
 AOBJ     := $(BUILD)/cyaes_adler.o
 BOBJ     := $(BUILD)/cyaes_batch_kernels.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
@@ -48,8 +57,24 @@ bounds: $(BOUNDS)
 $(BUILD):
 	mkdir -p $(BUILD)
 
-$(KOBJ): $(KSRC) $(HDRS) | $(BUILD)
+$(BUILD)/cyaes_kernels.o: $(KSRC) $(KHDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/cyaes_enc_kernels.o: $(ESRC) $(KHDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(SCHED_ENC) -c $< -o $@
+
+$(BUILD)/cyaes_dec_kernels.o: $(DSRC) $(KHDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(SCHED_DEC) -c $< -o $@
+
+# The three kernel objects of a variant build: $(call kvariant,NAME,DEFS)
+define kvariant
+	mkdir -p $(BUILD)/variants
+	$(HIPCC) $(HIPFLAGS) $(2) -c $(KSRC) -o $(BUILD)/variants/$(1).o
+	$(HIPCC) $(HIPFLAGS) $(SCHED_ENC) $(2) -c $(ESRC) -o $(BUILD)/variants/$(1)_enc.o
+	$(HIPCC) $(HIPFLAGS) $(SCHED_DEC) $(2) -c $(DSRC) -o $(BUILD)/variants/$(1)_dec.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/$(1).so $(BUILD)/variants/$(1).o \
+	  $(BUILD)/variants/$(1)_enc.o $(BUILD)/variants/$(1)_dec.o $(AOBJ) $(BOBJ) $(HOBJ)
+endef
 
 $(AOBJ): $(ASRC) include/cyaes_adler32.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -92,15 +117,11 @@ $(BUILD)/hostlink: tools/hostlink.hip | $(BUILD)
 $(BUILD)/microbench: tools/microbench.hip | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
-$(PROBE): $(KSRC) $(HDRS) $(HOBJ) $(AOBJ) $(BOBJ)
-	mkdir -p $(BUILD)/variants
-	$(HIPCC) $(HIPFLAGS) -DCYAES_CLOCK_PROBE=1 -c $(KSRC) -o $(BUILD)/variants/clockprobe.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(BUILD)/variants/clockprobe.o $(AOBJ) $(BOBJ) $(HOBJ)
+$(PROBE): $(KSRC) $(ESRC) $(DSRC) $(KHDRS) $(HOBJ) $(AOBJ) $(BOBJ)
+	$(call kvariant,clockprobe,-DCYAES_CLOCK_PROBE=1)
 
-$(BOUNDS): $(KSRC) $(HDRS) $(HOBJ) $(AOBJ) $(BOBJ)
-	mkdir -p $(BUILD)/variants
-	$(HIPCC) $(HIPFLAGS) -DCYAES_BOUNDS_CHECK=1 -c $(KSRC) -o $(BUILD)/variants/bounds.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(BUILD)/variants/bounds.o $(AOBJ) $(BOBJ) $(HOBJ)
+$(BOUNDS): $(KSRC) $(ESRC) $(DSRC) $(KHDRS) $(HOBJ) $(AOBJ) $(BOBJ)
+	$(call kvariant,bounds,-DCYAES_BOUNDS_CHECK=1)
 
 # Bitsliced decrypt prototype (measurement tool)
 $(BUILD)/bitslice: tools/bitslice.hip tools/bitslice_gen.h $(LIB) | $(BUILD)
@@ -108,9 +129,7 @@ $(BUILD)/bitslice: tools/bitslice.hip tools/bitslice_gen.h $(LIB) | $(BUILD)
 
 # A/B variants: make variant NAME=x DEFS="-DFOO=1" -> build/variants/x.so
 variant: $(HOBJ) $(AOBJ) $(BOBJ) | $(BUILD)
-	mkdir -p $(BUILD)/variants
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(KSRC) -o $(BUILD)/variants/$(NAME).o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/$(NAME).so $(BUILD)/variants/$(NAME).o $(AOBJ) $(BOBJ) $(HOBJ)
+	$(call kvariant,$(NAME),$(DEFS))
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(MGPU) $(ORACLE)

@@ -1,0 +1,345 @@
+// cyaes_dec_kernels.hip -- gfx950 CBC decrypt of uniform contiguous batches,
+// one lane per block (k_decrypt_flat; cyr_rijndael.cpp:612-635 + _decryptBlock
+// :708-774).  Compiled with the max-ILP scheduler (Makefile SCHED_DEC): config
+// C decrypt -1.5 % (profiles/r03/ab_sched.txt); design notes in cyaes_kernels.hip
+// and DESIGN.md §3.3.
+
+#define CYAES_TU 2
+#include "cyaes_device.h"
+
+namespace cyaes {
+namespace {
+
+// ---- CBC decrypt, uniform contiguous batch: one lane per block ------------
+// The batch is one array of nblocks blocks; payload boundaries every bpp
+// blocks restart the chain at the IV.  Each wave owns the contiguous range
+// [w*bpw, (w+1)*bpw) (bpw a multiple of 64*R) and walks it in steps of 64*R
+// blocks: R rows of 64 lanes, decrypted together (R-way ILP).  BIG: bpp >= 64*R,
+// so a step holds at most one payload start and needs no division.
+// Per-wave walk state of k_decrypt_flat (kept in registers: passed by value
+// and returned, never through memory).
+struct FlatPos {
+    uint64_t bp;    // payload of the step's first block
+    uint32_t bpos;  // its position in the payload
+};
+
+// Position of row k's block in its payload (r) and the payload index (p).
+template <bool BIG>
+__device__ __forceinline__ void flat_position(const DecArgs& a, FlatPos ps, uint32_t lane, int k, uint32_t& r,
+                                              uint64_t& p) {
+    const uint32_t lpos = ps.bpos + 64 * k + lane;
+    const uint32_t bpp = a.bpp.d;
+    if (BIG) {
+        r = min(lpos, lpos - bpp);
+        p = ps.bp + (lpos >= bpp ? 1 : 0);
+    } else {
+        const uint32_t q = fastdiv(lpos, a.bpp);
+        r = lpos - q * bpp;
+        p = ps.bp + q;
+    }
+}
+
+// Loads the R rows of the step at `base` (c); partial steps also load each
+// block's predecessor (pv), full steps take it from the neighbour lane.
+// FULL: all 64*R blocks are in range (every step but possibly the batch's
+// last), so loads are unguarded and use immediate offsets off one lane pointer.
+template <bool FULL>
+__device__ __forceinline__ void flat_load(const DecArgs& a, uint32_t lane, uint64_t base, uint64_t end,
+                                          uint4 (&c)[kDecRows], uint4 (&pv)[kDecRows]) {
+    constexpr int R = kDecRows;
+    const Ext ie = ext(a.in, 16 * a.nblocks);
+    if (FULL) {
+        const uint8_t* g0 = a.in + 16 * (base + lane);
+#pragma unroll
+        for (int k = 0; k < R; k++) c[k] = LD16(g0 + 1024 * k, ie);
+        // pv comes from the neighbour lane in flat_step (DPP), not from memory
+    } else {  // last, partial step of the batch: clamp reads into range
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const uint64_t g = min(base + 64 * k + lane, end - 1);
+            c[k] = LD16(a.in + 16 * g, ie);
+            // The predecessor of block g (lane 0 of row 0 reads its own block:
+            // the carry replaces it).  Block 0 has none: a 1-block batch (end
+            // == 1) clamps every lane to g = 0, and g - 1 would read 16 B before
+            // the buffer (r02 fault hunt, VERDICT r02 "What's weak" 1).  Block
+            // 0 is a payload start, so its pv is the IV in flat_step anyway.
+            const uint64_t back = (k == 0 && lane == 0) ? 0u : 1u;
+            pv[k] = LD16(a.in + 16 * (g >= back ? g - back : 0u), ie);
+        }
+    }
+}
+
+template <bool KEYED, bool BIG, bool FULL, bool IV>
+__device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, uint32_t lo, uint32_t lane,
+                                           uint64_t base, uint64_t end, FlatPos ps, uint4 carry,
+                                           uint32_t (&dk0)[44], uint32_t& dk_id, const uint4 (&c)[kDecRows],
+                                           uint4 (&pv)[kDecRows], const uint32_t (&rk)[kDecRows]) {
+    constexpr int R = kDecRows;
+    const Ext oe = ext(a.out, 16 * a.nblocks);
+    const Ext iv_in_e = iv_ext(a.iv_in, a.npayloads), iv_out_e = iv_ext(a.iv_out, a.npayloads);
+    if (FULL) {
+        // Predecessor blocks from the neighbour lane (DPP wave_shr:1), lane 0's
+        // from the row before (or the carry): no second load of C[i-1]
+        // (A/B: -4.8 % decrypt time vs the load at offset -16).  Every load of
+        // the step is then the lane's own block, which its store needs anyway,
+        // so in-place steps need no drain.
+        pv[0] = shr1(c[0], carry);
+#pragma unroll
+        for (int k = 1; k < R; k++)
+            pv[k] = shr1(c[k], make_uint4(rl63(c[k - 1].x), rl63(c[k - 1].y), rl63(c[k - 1].z), rl63(c[k - 1].w)));
+    } else {
+        if (lane == 0) pv[0] = carry;
+        if (a.inplace) drain_loads();  // pv loads read neighbours' blocks
+    }
+    // Chain restarts at payload starts inside this step.
+    if (BIG) {
+        const uint32_t fo = ps.bpos == 0 ? 0u : a.bpp.d - ps.bpos;  // offset of the payload start, if < 64R
+        // On a partial last step the "next payload" may start at or past the
+        // batch's end: then it does not exist, and iv_in[pf] would read 16 B
+        // past the IV array (VERDICT r02 "What's weak" 1).
+        if (fo < 64u * R && (FULL || base + fo < end)) {
+            const uint64_t pf = ps.bp + (ps.bpos == 0 ? 0 : 1);
+            const uint4 ivv = (IV && a.iv_in) ? LD16(a.iv_in + 16 * pf, iv_in_e) : default_iv();
+#pragma unroll
+            for (int k = 0; k < R; k++)
+                if ((fo >> 6) == (uint32_t)k && lane == (fo & 63u)) pv[k] = ivv;
+        }
+    } else if (!IV || !a.iv_in) {  // chains restart at DefaultIV: a select on the lane's tracked position
+#pragma unroll
+        for (int k = 0; k < R; k++)
+            if (rk[k] == 0) pv[k] = default_iv();
+    } else {
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            uint32_t r;
+            uint64_t p;
+            flat_position<BIG>(a, ps, lane, k, r, p);
+            if (r == 0) {
+                const bool valid = FULL || base + 64 * k + lane < end;
+                pv[k] = valid ? LD16(a.iv_in + 16 * p, iv_in_e) : default_iv();
+            }
+        }
+    }
+    if (IV && a.iv_out) {  // final chain block of each payload ending in this step
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            uint32_t r;
+            uint64_t p;
+            flat_position<BIG>(a, ps, lane, k, r, p);
+            if (r == a.bpp.d - 1 && (FULL || base + 64 * k + lane < end)) ST16(a.iv_out + 16 * p, iv_out_e, c[k]);
+        }
+    }
+    uint4 d[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) d[k] = pv[k];
+    if (!KEYED) {
+        dec_cbc<R>(lds, lo, dk0, c, d);  // all R rows per LDS round trip (A/B: ~1% over 2 rows)
+    } else {
+        uint32_t kid[R];
+        bool valid[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            uint32_t r;
+            uint64_t p;
+            flat_position<BIG>(a, ps, lane, k, r, p);
+            valid[k] = FULL || base + 64 * k + lane < end;
+            kid[k] = key_index(a.keys, p, a.npayloads, valid[k], a.status);
+        }
+        // Sessions are contiguous runs of payloads (config D: 256 x 92 blocks),
+        // so nearly every full step has one key: decrypt all R rows together
+        // under it (R-way ILP), as the unkeyed path does.  Otherwise fall back
+        // to a per-row waterfall over the keys present.
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(kid[0]);
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < R; k++) same = same && kid[k] == k0;
+        const bool uniform = FULL && __ballot(!same) == 0;
+        if (uniform) {
+            // dk0 keeps the last session's schedule (SGPRs) across steps: a
+            // session spans ~92 steps in config D
+            if (k0 != dk_id) {
+                load_sched(a.keys, k0, 1, dk0);
+                dk_id = k0;
+            }
+            dec_cbc<R>(lds, lo, dk0, c, d);
+        } else {
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                bool pending = valid[k];
+                while (true) {  // waterfall over the distinct keys of this row
+                    const uint64_t m = __ballot(pending);
+                    if (m == 0) break;
+                    const uint32_t ku = __builtin_amdgcn_readlane(kid[k], __builtin_ctzll(m));
+                    if (pending && kid[k] == ku) {
+                        pending = false;
+                        uint32_t dk[44];
+                        load_sched(a.keys, ku, 1, dk);
+                        const uint4 cc[1] = {c[k]};
+                        uint4 dd[1] = {d[k]};
+                        dec_cbc<1>(lds, lo, dk, cc, dd);
+                        d[k] = dd[0];
+                    }
+                }
+            }
+        }
+    }
+    if (FULL) {
+        uint8_t* o0 = a.out + 16 * (base + lane);
+#pragma unroll
+        for (int k = 0; k < R; k++) ST16(o0 + 1024 * k, oe, d[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < R; k++)
+            if (base + 64 * k + lane < end) ST16(a.out + 16 * (base + 64 * k + lane), oe, d[k]);
+    }
+    return make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));  // next carry
+}
+
+// SESS: sessions of payloads_per_key payloads that are whole steps long
+// (a.sess_blocks, a multiple of 64 * R; config D: 256 x 92 blocks): no step
+// straddles two sessions, so the unkeyed step runs under a schedule chosen per
+// step from the scalar block position, and no lane computes a key index.
+// IV = false: no IV arrays (the relay's calls, cyr_rijndael.cpp:612 with iv =
+// nullptr); the IV code and the payload-index tracking compile out, which
+// keeps the SGPR budget of the round loop (with them, the !BIG SESS kernel
+// scheduled its rounds with 321 s_waitcnt per 640 LDS reads against 173).
+template <bool KEYED, bool BIG, bool SESS, bool IV>
+__global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
+    constexpr int R = kDecRows;
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
+    fill_dec_image(lds_words, a.tables);
+    unsigned int* leadp = &g_dec_lead[blockIdx.x % kLeadSlots];
+    if (threadIdx.x == 0) *leadp = 0;
+    uint32_t prog = 0;
+    __syncthreads();
+    CLOCK_PROBE(1);
+    const uint64_t wave =
+        (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t begin = wave * a.blocks_per_wave;
+    if (begin >= a.nblocks) return;
+    const char* lds = reinterpret_cast<const char*>(lds_words);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lo = dec_lo(threadIdx.x);
+    const uint64_t end = min(begin + a.blocks_per_wave, a.nblocks);
+    FlatPos ps;
+    ps.bp = begin / a.bpp.d;
+    ps.bpos = (uint32_t)(begin - ps.bp * a.bpp.d);
+    uint4 carry = make_uint4(0, 0, 0, 0);  // C[base-1]
+    if (ps.bpos != 0)  // (begin >= 1 here)
+        carry = a.boundary ? LD16(a.boundary + wave, ext(a.boundary, 16ull * gridDim.x * (kDecThreads / 64)))
+                           : LD16(a.in + 16 * (begin - 1), ext(a.in, 16 * a.nblocks));
+    uint32_t dk0[44];
+    uint32_t dk_id = 0;  // KEYED: session whose schedule dk0 holds (~0u: none yet)
+    uint32_t sess = 0;   // SESS: session of the current step; it ends at block sess_next
+    uint64_t sess_next = 0;
+    if (SESS) {
+        sess = (uint32_t)(begin / a.sess_blocks);
+        sess_next = (uint64_t)(sess + 1) * a.sess_blocks;
+        load_sched(a.keys, sess, 1, dk0);
+    } else if (!KEYED) {
+        load_sched(a.keys, 0, 1, dk0);
+    } else {
+        dk_id = ~0u;
+    }
+    // !BIG: each lane tracks its rows' positions in their payloads, advanced
+    // by step_r per step (one add and a min instead of a division per row;
+    // A/B: config B decrypt ...).
+    uint32_t rk[R];
+    if (!BIG) {
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const uint32_t lpos = ps.bpos + 64 * k + lane;
+            rk[k] = lpos - fastdiv(lpos, a.bpp) * a.bpp.d;
+        }
+    }
+    uint64_t base = begin;
+    uint4 c[R], pv[R];
+    if (base + 64 * R <= end) flat_load<true>(a, lane, base, end, c, pv);
+    // SESS: an outer loop over the wave's sessions, the steps of one session
+    // inside it, so the schedule is invariant in the inner loop.  (Re-loading
+    // it inside the step loop made the compiler schedule the rounds with 321
+    // s_waitcnt per 640 LDS reads against 173.)
+    while (base + 64 * R <= end) {
+        uint64_t stop = end;
+        if (SESS) {
+            if (base >= sess_next) {  // (make_keysel checked every session is in the table)
+                sess++;
+                sess_next += a.sess_blocks;
+                load_sched(a.keys, sess, 1, dk0);
+            }
+            stop = min(end, sess_next);  // sessions are whole steps: base reaches sess_next exactly
+        }
+        for (; base + 64 * R <= stop; base += 64 * R) {
+            // (Issuing the next step's loads before this step's rounds measured ~1 %
+            // slower: the LDS binds, and the other 15 waves hide the loads.)
+            carry = flat_step<KEYED, BIG, true, IV>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv, rk);
+            if (base + 128 * R <= end) flat_load<true>(a, lane, base + 64 * R, end, c, pv);
+            prio_feedback(leadp, ++prog, kDecPrioDiv);
+            ps.bpos += a.step_r;
+            ps.bp += a.step_q;
+            if (ps.bpos >= a.bpp.d) { ps.bpos -= a.bpp.d; ps.bp++; }
+            if (!BIG) {
+#pragma unroll
+                for (int k = 0; k < R; k++) {
+                    const uint32_t t = rk[k] + a.step_r;  // < 2 bpp
+                    rk[k] = min(t, t - a.bpp.d);
+                }
+            }
+        }
+        if (!SESS) break;
+    }
+    if (base < end) {
+        if (SESS && base >= sess_next) load_sched(a.keys, sess + 1, 1, dk0);
+        flat_load<false>(a, lane, base, end, c, pv);
+        flat_step<KEYED, BIG, false, IV>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv, rk);
+    }
+}
+
+// In-place flat decrypt: snapshot C[begin-1] of every wave range before any
+// wave overwrites it.
+__global__ void k_boundary_snapshot(const uint4* in, uint64_t nblocks, uint64_t bpw, uint64_t nwaves, Fastdiv bpp,
+                                    uint4* boundary) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwaves) return;
+    const uint64_t begin = w * bpw;
+    if (begin == 0 || begin >= nblocks) return;
+    if (begin % bpp.d != 0)
+        ST16(boundary + w, ext(boundary, 16 * nwaves), LD16(in + (begin - 1), ext(in, 16 * nblocks)));
+}
+
+}  // namespace
+
+hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream) {
+    const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
+    const bool big = a.bpp.d >= 64u * kDecRows;
+    const dim3 g(grid), b(kDecThreads);
+    const bool sess = a.sess_blocks != 0;  // keyed by step-aligned sessions: the unkeyed step per session
+    const bool iv = a.iv_in != nullptr || a.iv_out != nullptr;  // (the runtime sets sess only without IVs)
+    if (sess && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, true, false>), g, b, 0, stream, a);
+    else if (sess) hipLaunchKernelGGL((k_decrypt_flat<false, false, true, false>), g, b, 0, stream, a);
+    else if (keyed && big) hipLaunchKernelGGL((k_decrypt_flat<true, true, false, true>), g, b, 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true, false, false, true>), g, b, 0, stream, a);
+    else if (big && iv) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, true>), g, b, 0, stream, a);
+    else if (big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false>), g, b, 0, stream, a);
+    else if (iv) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, true>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false>), g, b, 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_boundary_snapshot(const uint8_t* in, uint64_t nblocks, uint64_t blocks_per_wave, uint64_t nwaves,
+                                    Fastdiv bpp, uint4* boundary, hipStream_t stream) {
+    const int threads = 256;
+    const int grid = (int)((nwaves + threads - 1) / threads);
+    hipLaunchKernelGGL(k_boundary_snapshot, dim3(grid), dim3(threads), 0, stream,
+                       reinterpret_cast<const uint4*>(in), nblocks, blocks_per_wave, nwaves, bpp, boundary);
+    return hipGetLastError();
+}
+
+#if CYAES_BOUNDS_CHECK
+int bounds_read_dec(unsigned long long* rec4, unsigned int* lines) { return read_bounds_local(rec4, lines); }
+#endif
+#if CYAES_CLOCK_PROBE
+int probe_read_dec(unsigned long long* out8) { return read_probe_local(out8); }
+#endif
+
+}  // namespace cyaes

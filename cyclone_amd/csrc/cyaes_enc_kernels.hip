@@ -1,0 +1,187 @@
+// cyaes_enc_kernels.hip -- gfx950 CBC encrypt, one lane per payload chain
+// (k_encrypt; cyr_rijndael.cpp:588-609 + _encryptBlock :638-705).  Compiled
+// with the iterative ILP scheduler (Makefile SCHED_ENC): config C encrypt
+// -1.5 %, B -1.3 % (profiles/r03/ab_sched.txt); the design notes are in
+// cyaes_kernels.hip and DESIGN.md §3.2.
+
+#define CYAES_TU 1
+#include "cyaes_device.h"
+
+namespace cyaes {
+namespace {
+
+// ---- CBC encrypt: one lane per payload chain (cyr_rijndael.cpp:588-609) ----
+// RUNS (uniform batches of short payloads, no IV arrays): a lane's work item
+// is a run of a.run consecutive payloads, contiguous in memory, encrypted as
+// one block stream whose chain restarts at DefaultIV every bpp blocks
+// (relay_local.cpp:206 passes no IV, so every payload is its own chain).  The
+// next-chunk prefetch then never stops at a payload boundary: a lane of
+// config B (1,472-B payloads) streams 368 blocks instead of four 92-block
+// payloads, each of which started on an exposed load and ended in a 4-block
+// tail.  The restart test is on wave-uniform block counters (scalar).
+// SESS (uniform batches keyed by sessions of payloads_per_key payloads that
+// are whole waves long, config D): a wave's work items all lie in one session,
+// so its key comes from the scalar position, per wave, in SGPRs -- the
+// unkeyed code path, no per-lane key index and no waterfall.  The grid has a
+// lane per work item (not persistent).
+template <bool RAGGED, bool KEYED, bool RUNS, bool SESS>
+__global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
+    fill_region(lds_words, a.tables, a.tables + 512, blockDim.x);              // TL1 | TL3
+    fill_region(lds_words + 16384, a.tables + 256, a.tables + 768, blockDim.x);  // TL2 | TL4
+    __shared__ uint32_t lead;  // prio_feedback
+    if (threadIdx.x == 0) lead = 0;
+    uint32_t prog = 0;
+    __syncthreads();
+    CLOCK_PROBE(0);
+    const char* lds = reinterpret_cast<const char*>(lds_words);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
+    // Block size: kEncThreads for big batches; fewer for small ones, so that
+    // few chains spread over many CUs (cyaes_runtime.cpp, wave_shape).
+    const uint64_t wstride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t wbase0 = (uint64_t)blockIdx.x * blockDim.x + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+    const Ext iv_in_e = iv_ext(a.iv_in, a.npayloads), iv_out_e = iv_ext(a.iv_out, a.npayloads);
+    const uint32_t R = RUNS ? a.run : 1u;  // payloads per work item
+    const uint32_t bpp = a.payload_bytes >> 4;
+    const uint64_t nwork = RUNS ? (a.npayloads + R - 1) / R : a.npayloads;
+    uint32_t ek[44];
+    // One schedule per wave, loaded before the loop: the whole batch's, or
+    // (SESS) the wave's session's, from its scalar position.  A SESS grid covers
+    // the batch in one pass (one work item per lane, the runtime sizes the
+    // grid), so the loop body runs once.  Re-loading ek inside the loop instead
+    // made the compiler schedule the round loop with 57 s_waitcnt per 160 LDS
+    // reads against 44 (config D encrypt 1.11 ms against B's 1.09).
+    if (SESS) load_sched(a.keys, wbase0 < nwork ? (uint32_t)(wbase0 * R / a.sess_payloads) : 0u, 0, ek);
+    else if (!KEYED) load_sched(a.keys, 0, 0, ek);
+
+    for (uint64_t wbase = wbase0; wbase < nwork; wbase += wstride) {
+        const uint64_t w = wbase + lane;
+        const bool active = w < nwork;
+        const uint64_t p = RUNS ? w * R : w;  // (first) payload of the work item
+        uint64_t off;
+        uint32_t nb;
+        if (RAGGED) {
+            off = active ? LD8(a.offsets + p, ext(a.offsets, 8 * a.npayloads)) : 0;
+            nb = active ? (LD4(a.nbytes + p, ext(a.nbytes, 4 * a.npayloads)) >> 4) : 0;
+        } else {
+            off = p * (uint64_t)a.payload_bytes;
+            nb = active ? (RUNS ? (uint32_t)min<uint64_t>(R, a.npayloads - p) * bpp : bpp) : 0;
+        }
+        // RUNS + KEYED: the runtime makes runs divide payloads_per_key, so the run is one session
+        const uint32_t kid = KEYED ? key_index(a.keys, p, a.npayloads, active, a.status) : 0u;
+        bool pending = active;
+        while (true) {  // waterfall over the distinct keys of this wave
+            const uint64_t m = __ballot(pending);
+            if (m == 0) break;
+            const uint32_t ku = KEYED ? __builtin_amdgcn_readlane(kid, __builtin_ctzll(m)) : 0u;
+            if (pending && (!KEYED || kid == ku)) {
+                pending = false;
+                if (KEYED) load_sched(a.keys, ku, 0, ek);
+                uint4 c = a.iv_in ? LD16(a.iv_in + 16 * p, iv_in_e) : default_iv();
+                const uint8_t* src = a.in + off;  // ragged: 4-B aligned
+                uint8_t* dst = a.out + off;
+                const Ext se = ext(src, 16ull * nb), de = ext(dst, 16ull * nb);  // this work item's bytes
+                uint32_t nr = bpp;  // RUNS: block index of the next chain restart (a payload start)
+                uint32_t i = 0;
+                uint4 b[8];
+                if (nb >= 8) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) b[j] = ldb<RAGGED>(src, j, se);
+                }
+                bool have_tail = false;  // b[8 - (nb - i), 8) already hold the last partial chunk
+                for (; i + 8 <= nb; i += 8) {
+                    const bool more = i + 16 <= nb;
+                    const bool tail = !more && i + 8 < nb;  // partial last chunk
+                    // Next chunk's loads in flight during this chunk's rounds (-8 %
+                    // encrypt time).  One set of 8 loads for both cases: a partial
+                    // last chunk loads the payload's last 8 blocks (its tail then
+                    // sits at the top of bn).  With every bn[j] defined on this
+                    // path the compiler no longer waits for this chunk's stores
+                    // (s_waitcnt vmcnt(0)) before the next chunk's loads; it waits
+                    // only for the loads (profiles/r02/ab_onepf.txt).
+                    uint4 bn[8];
+                    if (more || tail) {
+                        const uint8_t* nsrc = src + 16ull * (more ? i + 8 : nb - 8);
+#pragma unroll
+                        for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(nsrc, j, se);
+                    }
+                    prio_feedback(&lead, ++prog, kEncPrioDiv);
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        if (RUNS && i + j == nr) {  // next payload of the run: a new chain
+                            c = default_iv();
+                            nr += bpp;
+                        }
+                        uint32_t s0 = xor3(c.x, b[j].x, ek[0]), s1 = xor3(c.y, b[j].y, ek[1]);
+                        uint32_t s2 = xor3(c.z, b[j].z, ek[2]), s3 = xor3(c.w, b[j].w, ek[3]);
+                        enc_block(lds, lo, ek, s0, s1, s2, s3);
+                        c = make_uint4(s0, s1, s2, s3);
+                        b[j] = c;
+                    }
+                    uint8_t* const dchunk = dst + 16ull * i;  // one address, immediate offsets (ragged too)
+#pragma unroll
+                    for (int j = 0; j < 8; j++) stb<RAGGED>(dchunk, j, b[j], de);  // (nt stores measured 3.6x slower)
+                    if (more || tail) {
+#pragma unroll
+                        for (int j = 0; j < 8; j++) b[j] = bn[j];
+                    }
+                    have_tail = tail;
+                }
+                if (have_tail) {  // the tail's nb - i blocks sit in b[8 - (nb - i), 8): move them down to b[0]
+#pragma unroll
+                    for (int sft = 1; sft < 8; sft++) {
+                        if (sft <= 8 - (int)(nb - i)) {
+#pragma unroll
+                            for (int j = 0; j < 7; j++) b[j] = b[j + 1];
+                        }
+                    }
+                }
+                for (; i < nb; i++) {  // partial last chunk: from b (prefetched) or loaded here
+                    const uint4 v = have_tail ? b[0] : ldb<RAGGED>(src, i, se);
+#pragma unroll
+                    for (int j = 0; j < 7; j++) b[j] = b[j + 1];
+                    if (RUNS && i == nr) {
+                        c = default_iv();
+                        nr += bpp;
+                    }
+                    uint32_t s0 = xor3(c.x, v.x, ek[0]), s1 = xor3(c.y, v.y, ek[1]);
+                    uint32_t s2 = xor3(c.z, v.z, ek[2]), s3 = xor3(c.w, v.w, ek[3]);
+                    enc_block(lds, lo, ek, s0, s1, s2, s3);
+                    c = make_uint4(s0, s1, s2, s3);
+                    stb<RAGGED>(dst, i, c, de);
+                }
+                if (a.iv_out) ST16(a.iv_out + 16 * p, iv_out_e, c);  // (RUNS: no IV arrays)
+            }
+        }
+        if (SESS) break;  // one pass (above)
+    }
+}
+
+}  // namespace
+
+hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t stream) {
+    const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
+    const bool ragged = a.offsets != nullptr;
+    const dim3 g(grid), b(threads);
+    const bool runs = !ragged && a.run > 1;
+    const bool sess = !ragged && a.sess_payloads != 0;  // keyed by whole-wave sessions: the unkeyed body per session
+    if (ragged && keyed) hipLaunchKernelGGL((k_encrypt<true, true, false, false>), g, b, 0, stream, a);
+    else if (ragged) hipLaunchKernelGGL((k_encrypt<true, false, false, false>), g, b, 0, stream, a);
+    else if (sess && runs) hipLaunchKernelGGL((k_encrypt<false, false, true, true>), g, b, 0, stream, a);
+    else if (sess) hipLaunchKernelGGL((k_encrypt<false, false, false, true>), g, b, 0, stream, a);
+    else if (runs && keyed) hipLaunchKernelGGL((k_encrypt<false, true, true, false>), g, b, 0, stream, a);
+    else if (runs) hipLaunchKernelGGL((k_encrypt<false, false, true, false>), g, b, 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_encrypt<false, true, false, false>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((k_encrypt<false, false, false, false>), g, b, 0, stream, a);
+    return hipGetLastError();
+}
+
+#if CYAES_BOUNDS_CHECK
+int bounds_read_enc(unsigned long long* rec4, unsigned int* lines) { return read_bounds_local(rec4, lines); }
+#endif
+#if CYAES_CLOCK_PROBE
+int probe_read_enc(unsigned long long* out8) { return read_probe_local(out8); }
+#endif
+
+}  // namespace cyaes

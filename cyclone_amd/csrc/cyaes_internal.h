@@ -1,5 +1,7 @@
-// cyaes_internal.h -- shared between the gfx950 kernels (cyaes_kernels.hip)
-// and the host runtime (cyaes_runtime.cpp).  Not part of the public ABI.
+// cyaes_internal.h -- shared between the gfx950 kernels (cyaes_kernels.hip,
+// cyaes_enc_kernels.hip, cyaes_dec_kernels.hip; device helpers in
+// cyaes_device.h) and the host runtime (cyaes_runtime.cpp).  Not part of the
+// public ABI.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -112,7 +114,7 @@ struct DecArgs {
     uint64_t sess_blocks;     // flat kernel: blocks per payloads_per_key session when a multiple of a step, else 0
 };
 
-// Launchers (cyaes_kernels.hip).  All asynchronous on `stream`.
+// Launchers (cyaes_*kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t stream);
 // Four lanes per chain (latency-bound batches; threads a multiple of 64).
 hipError_t launch_encrypt_quad(const EncArgs& a, int grid, int threads, hipStream_t stream);
@@ -125,6 +127,13 @@ hipError_t launch_key_expand(const uint8_t* d_keys, uint32_t nkeys, const uint8_
 hipError_t launch_fill_synthetic(uint8_t* buf, uint64_t p0, uint64_t npayloads, uint32_t payload_bytes,
                                  uint64_t seed, hipStream_t stream);
 hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long* out2, hipStream_t stream);
+// Variant builds: read and clear the debug records of the encrypt / decrypt
+// kernel TUs (CYAES_BOUNDS_CHECK: 4 words + the per-position miss counts;
+// CYAES_CLOCK_PROBE: 8 words).  cyaes_debug_bounds / _probe sum them.
+int bounds_read_enc(unsigned long long* rec4, unsigned int* lines);
+int bounds_read_dec(unsigned long long* rec4, unsigned int* lines);
+int probe_read_enc(unsigned long long* out8);
+int probe_read_dec(unsigned long long* out8);
 
 // Batching adapter request descriptor (cyaes_batcher.cpp builds them in pinned
 // memory, cyaes_batch_kernels.hip reads them).  src / dst are DEVICE

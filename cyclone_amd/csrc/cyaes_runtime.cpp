@@ -246,9 +246,10 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     a.status = ctx->d_status;
     a.inplace = in == out;
     // Sessions of payloads_per_key payloads that are whole steps long: every
-    // step lies in one session (the kernel picks its schedule per step).
+    // step lies in one session (the kernel picks its schedule per step).  Only
+    // without IV arrays (the SESS kernels compile the IV code out).
     const uint64_t sess_blocks = (uint64_t)ppk * bpp;
-    if (!key_idx && ppk && sess_blocks % step == 0) a.sess_blocks = sess_blocks;
+    if (!key_idx && ppk && sess_blocks % step == 0 && !iv_in && !iv_out) a.sess_blocks = sess_blocks;
     if (in == out && nwaves > 1) {
         st = boundary.get(ctx->pool, nwaves * sizeof(uint4), stream);
         if (st) return st;

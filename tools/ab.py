@@ -4,6 +4,8 @@
 
 usage: python tools/ab.py build/variants/a.so build/variants/b.so [--rounds 6] [--payloads N]
        [--payload-bytes B] [--ppk K]   (--ppk: sessions of K payloads, config D's keys)
+       [--relay]   (the payloads inside relay packets, 12-B headers, stride B + 12, ragged kernels
+                    in place, as bench.py's relay_stream)
 A library may carry context settings: path:NAME=VALUE[:NAME=VALUE] sets those
 environment variables while its context is created (e.g. the same library
 twice, once with CYAES_ENC_RUN=1).
@@ -27,6 +29,7 @@ def main():
     ap.add_argument("--payload-bytes", type=int, default=65536)
     ap.add_argument("--ppk", type=int, default=0, help="payloads per session key (0: one key)")
     ap.add_argument("--key-idx", action="store_true", help="with --ppk: the same sessions as a per-payload index array")
+    ap.add_argument("--relay", action="store_true", help="relay packet stream in place (ragged kernels)")
     args = ap.parse_args()
     import torch
     import cyclone_amd as ca
@@ -59,6 +62,8 @@ def main():
     rt = torch.empty_like(pt)
     ctxs[0].fill_synthetic(pt, 0, n, pb, 0x5EEDC1C1)
     s = torch.cuda.current_stream()
+    if args.relay:
+        return relay(args, ctxs, pt, torch, s)
     kidx = None
     if args.key_idx and args.ppk:
         kidx = (torch.arange(n, dtype=torch.int64, device="cuda") // args.ppk).to(torch.int32)
@@ -94,6 +99,45 @@ def main():
             if waves:
                 print("    %s clock %.3f GHz, mean wave %.3f ms, max wave %.3f ms (per launch)" % (
                     kind, cyc / tick * 0.1, tick / waves / 1e5, tmax / len(v) / 1e5))
+
+
+def relay(args, ctxs, pt, torch, s):
+    """Interleaved in-place ragged encrypt + decrypt of a relay packet stream."""
+    n, pb = args.payloads, args.payload_bytes
+    hdr, stride = 12, pb + 12
+    buf = torch.full((n * stride + 16,), 0xA5, dtype=torch.uint8, device="cuda")
+    view = buf[: n * stride].view(n, stride)
+    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride + hdr
+    d_nb = torch.full((n,), pb, dtype=torch.int32, device="cuda")
+    times = {p: {"enc": [], "dec": []} for p in args.libs}
+    digests = {}
+    for r in range(args.rounds + 1):
+        for path, c in zip(args.libs, ctxs):
+            view[:, hdr:hdr + pb] = pt.view(n, pb)
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record(s)
+            c.encrypt_ragged(buf, buf, d_off, d_nb, n, stream=s.cuda_stream)
+            e[1].record(s)
+            if r == 0:
+                torch.cuda.synchronize()
+                dct = c.digest(buf, n * stride)
+            c.decrypt_ragged(buf, buf, d_off, d_nb, n, stream=s.cuda_stream)
+            e[2].record(s)
+            torch.cuda.synchronize()
+            if r == 0:
+                ok = bool(torch.equal(view[:, hdr:hdr + pb].reshape(-1), pt)) and bool((view[:, :hdr] == 0xA5).all())
+                digests[path] = (dct, ok)
+                continue
+            times[path]["enc"].append(e[0].elapsed_time(e[1]))
+            times[path]["dec"].append(e[1].elapsed_time(e[2]))
+    ref = digests[args.libs[0]][0]
+    for path in args.libs:
+        t = times[path]
+        print("%-40s relay enc med %.3f min %.3f | dec med %.3f min %.3f | %s" % (
+            path.replace(ROOT + "/", "").replace("cyclone_amd/", ""), statistics.median(t["enc"]), min(t["enc"]),
+            statistics.median(t["dec"]), min(t["dec"]),
+            ("same-output" if digests[path][0] == ref else "OUTPUT DIFFERS") +
+            ("" if digests[path][1] else " ROUND TRIP FAILED")))
 
 
 def probe(ctx, sink):

@@ -76,8 +76,9 @@ for step in "$@"; do
       IFS=: read -r _ A B ARGS <<< "$step"
       L="build/variants/$A.so build/variants/$B.so"
       RL="build/variants/$B.so build/variants/$A.so"
-      run ab_${A}_vs_${B} 300 python tools/ab.py $L ${ARGS//,/ }
-      run ab_${B}_vs_${A} 300 python tools/ab.py $RL ${ARGS//,/ } ;;
+      T=$(echo "$ARGS" | tr -c 'A-Za-z0-9' '_')
+      run ab_${A}_vs_${B}_$T 300 python tools/ab.py $L ${ARGS//,/ }
+      run ab_${B}_vs_${A}_$T 300 python tools/ab.py $RL ${ARGS//,/ } ;;
     abenv:*)  # abenv:NAME=V[+NAME=V]:ARGS -- the product library against itself with those context settings
       IFS=: read -r _ ENVS ARGS <<< "$step"
       L="cyclone_amd/libcyaes.so cyclone_amd/libcyaes.so:${ENVS//+/:}"
