@@ -42,13 +42,18 @@ def main():
     layouts = [("contig_out", 0, pb, False), ("contig_inplace", 0, pb, True),
                ("hdr16_out", 16, pb + 16, False), ("hdr16_inplace", 16, pb + 16, True),
                ("hdr12_s1488_out", 12, pb + 16, False), ("hdr12_s1488_inplace", 12, pb + 16, True),
-               ("relay_out", 12, pb + 12, False), ("relay_inplace", 12, pb + 12, True)]
+               ("relay_out", 12, pb + 12, False), ("relay_inplace", 12, pb + 12, True),
+               # r03: alignment alone (contiguous payloads shifted off 16/32 B) vs stride alone
+               ("contig_off4_inplace", 4, pb, True), ("contig_off16_inplace", 16, pb, True),
+               ("contig_off32_inplace", 32, pb, True), ("s1536_off0_inplace", 0, 1536, True),
+               ("s1536_off12_inplace", 12, 1536, True), ("s1536_off16_inplace", 16, 1536, True)]
     if args.layouts:
         keep = args.layouts.split(",")
         layouts = [ly for ly in layouts if ly[0] in keep]
     for label, hdr, stride, inplace in layouts:
-        src = torch.zeros(n * stride + 16, dtype=torch.uint8, device="cuda")
-        src[: n * stride].view(n, stride)[:, hdr:hdr + pb] = pt.view(n, pb)
+        src = torch.zeros(n * stride + 64, dtype=torch.uint8, device="cuda")
+        fill = lambda: src[hdr: hdr + n * stride].view(n, stride)[:, :pb].copy_(pt.view(n, pb))
+        fill()
         dst = src if inplace else torch.zeros_like(src)
         off = torch.from_numpy(np.arange(n, dtype=np.uint64) * stride + hdr).to("cuda")
         ts = [[] for _ in ctxs]
@@ -56,7 +61,7 @@ def main():
         for r in range(args.rounds + 1):
             for k, ck in enumerate(ctxs):
                 if inplace:
-                    src[: n * stride].view(n, stride)[:, hdr:hdr + pb] = pt.view(n, pb)
+                    fill()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
                 ck.encrypt_ragged(src, dst, off, nb, n, stream=s.cuda_stream)
@@ -64,7 +69,7 @@ def main():
                 torch.cuda.synchronize()
                 if r:
                     ts[k].append(e0.elapsed_time(e1))
-                ok[k] = ok[k] and torch.equal(dst[: n * stride].view(n, stride)[:, hdr:hdr + pb].reshape(-1), ref)
+                ok[k] = ok[k] and torch.equal(dst[hdr: hdr + n * stride].view(n, stride)[:, :pb].reshape(-1), ref)
         for k, p in enumerate(libs):
             print("%-22s %8d x %5d B stride %5d: enc %.4f ms (min %.4f)  %s  %s" %
                   (label, n, pb, stride, statistics.median(ts[k]), min(ts[k]), "ok" if ok[k] else "MISMATCH",
