@@ -91,10 +91,60 @@ def parse():
                     help="1: also time config B's payloads as an in-place relay packet stream (offset 12)")
     ap.add_argument("--packet-cpu-sample", type=int, default=0,
                     help="packet configs: payloads in the CPU-baseline sample (0 = auto: the whole 1,472-B batch)")
+    ap.add_argument("--traffic", default="live", choices=["live", "file", "none"],
+                    help="roofline.traffic: live = rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over config C "
+                         "run as child processes in this run (rank 0, N=1); file = profiles/traffic.json")
     ap.add_argument("--packet-warmup", type=int, default=20,
                     help="untimed steps before each packet config (a 1,472-B step is ~2 ms; 20 cover the clock "
                          "ramp, profiles/r01/packet_warmup.txt)")
     return ap.parse_args()
+
+
+def live_traffic(timeout_s=150):
+    """HBM bytes per AES launch, measured now: two rocprofv3 --pmc passes
+    (FETCH_SIZE, WRITE_SIZE; one counter each, as MI355X_MICROARCH.md's
+    HBM section prescribes) over `bench.py --config C --steps 2`, each a child
+    process with its own time limit.  Corrections as tools/traffic.py: kB x1024,
+    FETCH_SIZE x2 on gfx950.  Returns ({"encrypt": bytes, "decrypt": bytes}, None)
+    or (None, reason)."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import traffic as tr
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    out = {}
+    with tempfile.TemporaryDirectory(prefix="cyaes_pmc_") as tmp:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C", "--steps", "2", "--warmup", "0",
+                   "--no-cpu", "--no-verify", "--no-clock", "--packet-configs", "none", "--relay-stream", "0",
+                   "--traffic", "none"]
+            env = dict(os.environ)
+            for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+                env.pop(k, None)
+            proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd=tmp, env=env,
+                                    start_new_session=True)
+            try:
+                proc.wait(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(proc.pid, signal.SIGKILL)
+                proc.wait()
+                return None, "rocprofv3 --pmc %s timed out" % counter
+            if proc.returncode != 0:
+                return None, "rocprofv3 --pmc %s exited %d" % (counter, proc.returncode)
+            try:
+                kb = tr.per_launch_kb(d, counter)
+            except SystemExit as e:
+                return None, str(e)
+            for kind, v in kb.items():
+                out.setdefault(kind, 0)
+                out[kind] += int(round(v * 1024 * (2 if counter == "FETCH_SIZE" else 1)))
+    return out, None
 
 
 def session_keys(n):
@@ -471,11 +521,27 @@ def main():
     roofline = dict(roof(enc_ms if dom == "encrypt" else dec_ms), kernel=dom, traffic=None,
                     ceiling=kern[dom]["ceiling"])
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    ftr = None
     if os.path.exists(tfile):
-        tr = json.load(open(tfile)).get("C" if args.config == "E" else args.config, {}).get(dom)
-        if tr:
-            roofline["traffic"] = tr.get("bytes_per_launch")
-            roofline["traffic_note"] = tr.get("note")
+        ftr = json.load(open(tfile)).get("C" if args.config == "E" else args.config, {}).get(dom)
+    live, why = (None, "not requested")
+    if args.traffic == "live" and rank == 0 and world == 1 and args.config in ("C", "E"):
+        log("hbm traffic: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (config C) ...")
+        live, why = live_traffic()
+    if live and dom in live:
+        algo = 2.0 * nbytes
+        roofline["traffic"] = live[dom]
+        roofline["traffic_note"] = ("measured in this run: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes (separate "
+                                    "child processes, bench.py --config C --steps 2), FETCH_SIZE x2 per the gfx950 "
+                                    "calibration, x1024 kB->B; per launch of the dominant kernel")
+        roofline["traffic_ratio"] = round(live[dom] / algo, 4)
+        for k in kern:
+            if k in live:
+                kern[k]["traffic"] = live[k]
+                kern[k]["traffic_ratio"] = round(live[k] / algo, 4)
+    elif ftr and args.traffic != "none":
+        roofline["traffic"] = ftr.get("bytes_per_launch")
+        roofline["traffic_note"] = "committed profiles/traffic.json (%s); " % (why,) + str(ftr.get("note"))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
