@@ -269,6 +269,8 @@ struct cyaes_batcher {
     std::condition_variable cv_submit, cv_free, cv_inflight, cv_flush;
     std::vector<Stage*> free_stages;
     std::deque<Stage*> inflight;
+    std::vector<Cb> run_cbs;    // completer: the callbacks of the batch being completed
+    std::vector<Seg> run_segs;
     bool builder_done = false;
     uint64_t completed = 0, batches = 0, bytes = 0, max_batch = 0, errors = 0;
     int first_error = CYAES_OK;
@@ -688,18 +690,35 @@ void cyaes_batcher::complete_loop() {
             });
         const int64_t t2 = now_ns();
         pc.copy_out += t2 - t1;
+        // The stage's outputs are out: hand it back to the builder now and run
+        // its callbacks from completer-owned lists (swapped with last batch's,
+        // so no allocation), so the GPU pipeline does not wait on callbacks.
+        // Batches still complete one after another, so each shard's callbacks
+        // keep their submission order.
+        run_cbs.swap(st->cbs);
+        run_segs.swap(st->segs);
+        st->cbs.clear();
+        st->segs.clear();
+        const uint64_t sbytes = st->bytes;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            free_stages.push_back(st);
+        }
+        cv_free.notify_one();
         // Callbacks: one job per shard run, in that shard's submission order.
         // Poll mode: requests without a callback go to their shard's queue in
         // one locked append per run.
         const bool poll = (cfg.flags & CYAES_BATCHER_POLL) != 0;
-        workers->run(st->segs.size(), [this, st, status, poll](size_t k) {
-            const Seg& g = st->segs[k];
+        const std::vector<Cb>& cbs = run_cbs;
+        const std::vector<Seg>& segs = run_segs;
+        workers->run(segs.size(), [this, &cbs, &segs, status, poll](size_t k) {
+            const Seg& g = segs[k];
             if (poll) {
                 thread_local std::vector<Done> out;
                 out.clear();
                 for (uint32_t i = g.begin; i < g.end; i++) {
-                    if (st->cbs[i].done) st->cbs[i].done(st->cbs[i].user, status);
-                    else out.push_back({st->cbs[i].user, status});
+                    if (cbs[i].done) cbs[i].done(cbs[i].user, status);
+                    else out.push_back({cbs[i].user, status});
                 }
                 if (!out.empty()) {
                     Shard& sh = shards[g.shard];
@@ -709,24 +728,22 @@ void cyaes_batcher::complete_loop() {
                 return;
             }
             for (uint32_t i = g.begin; i < g.end; i++)
-                if (st->cbs[i].done) st->cbs[i].done(st->cbs[i].user, status);
+                if (cbs[i].done) cbs[i].done(cbs[i].user, status);
         });
-        const size_t nreq = st->cbs.size();
+        const size_t nreq = cbs.size();
         pc.callbacks += now_ns() - t2;
         pc.batches++;
         pc.reqs += (int64_t)nreq;
         lk.lock();
         completed += nreq;
-        for (const Seg& g : st->segs) done_seq[g.shard] = std::max(done_seq[g.shard], g.last_seq);
+        for (const Seg& g : segs) done_seq[g.shard] = std::max(done_seq[g.shard], g.last_seq);
         batches++;
-        bytes += st->bytes;
+        bytes += sbytes;
         max_batch = std::max<uint64_t>(max_batch, nreq);
         if (status != CYAES_OK) {
             errors += nreq;
             if (first_error == CYAES_OK) first_error = status;
         }
-        free_stages.push_back(st);
-        cv_free.notify_one();
         cv_flush.notify_all();
     }
 }
@@ -818,6 +835,7 @@ int cyaes_batcher_create(const cyaes_batcher_config* cfg, cyaes_batcher** out) {
         s.cbs.reserve(kMaxReqs);
         b->free_stages.push_back(&s);
     }
+    b->run_cbs.reserve(kMaxReqs);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&b->d_keys), (uint64_t)b->key_cap * kSchedBytes);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->pipe, hipStreamNonBlocking);
     (void)hipSetDevice(dev_prev);

@@ -131,7 +131,7 @@ static double pct(std::vector<double>& v, double p) {
 
 int main(int argc, char** argv) {
     std::string op = "seal";
-    uint32_t size = 1472, threads = 8, window = 512, batch_mb = 32, delay_us = 100, workers = 8, inflight = 3, bulk = 1;
+    uint32_t size = 1472, threads = 8, window = 512, batch_mb = 32, delay_us = 100, workers = 4, inflight = 3, bulk = 1;
     uint32_t use_pool = 1, reopen_copy = 0;
     std::string submit_kind = "ptr", dump, complete = "callback";
     double seconds = 5;
