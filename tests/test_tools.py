@@ -1,0 +1,64 @@
+"""Host-side measurement plumbing (no GPU): the rocprofv3 counter parsing that
+bench.py's live roofline.traffic and tools/traffic.py share, and the
+corrections MI355X_MICROARCH.md's HBM section prescribes for gfx950
+(counters in kB, FETCH_SIZE counting half the bytes)."""
+import csv
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import traffic  # noqa: E402
+
+FIELDS = ["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"]
+
+
+def write_counters(d, rows):
+    os.makedirs(os.path.join(d, "host", "1234"), exist_ok=True)
+    with open(os.path.join(d, "host", "1234", "run_counter_collection.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=FIELDS)
+        w.writeheader()
+        for r in rows:
+            w.writerow(dict(zip(FIELDS, r)))
+
+
+def test_per_launch_kb_averages_per_dispatch_and_kernel(tmp_path):
+    enc = "void cyaes::(anonymous namespace)::k_encrypt<false, false, false, false>(cyaes::EncArgs)"
+    dec = "void cyaes::(anonymous namespace)::k_decrypt_flat<false, true, false, false>(cyaes::DecArgs)"
+    rows = [
+        # two encrypt launches, each reported as two per-XCD rows that sum
+        (1, enc, "FETCH_SIZE", 100.0), (1, enc, "FETCH_SIZE", 50.0),
+        (3, enc, "FETCH_SIZE", 200.0), (3, enc, "FETCH_SIZE", 250.0),
+        (2, dec, "FETCH_SIZE", 80.0),
+        (4, "k_fill_synthetic", "FETCH_SIZE", 1e9),  # not an AES kernel: ignored
+        (2, dec, "WRITE_SIZE", 5.0),                 # another counter: ignored here
+    ]
+    write_counters(str(tmp_path), rows)
+    kb = traffic.per_launch_kb(str(tmp_path), "FETCH_SIZE")
+    assert kb == {"encrypt": pytest.approx(300.0), "decrypt": pytest.approx(80.0)}
+
+
+def test_missing_counter_file_is_reported(tmp_path):
+    with pytest.raises(SystemExit):
+        traffic.per_launch_kb(str(tmp_path), "FETCH_SIZE")
+
+
+def test_traffic_json_corrections(tmp_path):
+    enc = "k_encrypt<false, false, false, false>"
+    dec = "k_decrypt_flat<false, true, false, false>"
+    fdir, wdir = str(tmp_path / "f"), str(tmp_path / "w")
+    algo_kb = traffic.ALGO / 1024
+    # FETCH reads half the bytes on gfx950: N/2 kB read + N kB written = the algorithmic 2N
+    write_counters(fdir, [(1, enc, "FETCH_SIZE", algo_kb / 4), (2, dec, "FETCH_SIZE", algo_kb / 4)])
+    write_counters(wdir, [(1, enc, "WRITE_SIZE", algo_kb / 2), (2, dec, "WRITE_SIZE", algo_kb / 2)])
+    out = str(tmp_path / "traffic.json")
+    sys.argv = ["traffic.py", fdir, wdir, "--out", out]
+    traffic.main()
+    import json
+    t = json.load(open(out))["C"]
+    for k in ("encrypt", "decrypt"):
+        assert t[k]["bytes_per_launch"] == traffic.ALGO
+        assert t[k]["ratio"] == 1.0
+        assert t[k]["fetch_bytes"] == traffic.ALGO // 2
