@@ -619,3 +619,55 @@ def test_poll_mode_completions_in_submission_order():
         b.unregister_pool(pid)
     finally:
         b.close()
+
+
+def test_slow_callbacks_keep_order_and_flush_semantics():
+    """The completion thread hands a stage back to the builder before running
+    its callbacks (r03).  With slow callbacks over many small batches, each
+    submitting thread still sees its callbacks in submission order, outputs are
+    the oracle's, and flush() returns only after every earlier callback has
+    returned."""
+    import time
+    b = ca.Batcher(0, max_batch_bytes=32 << 10, max_delay_us=20, inflight=3)
+    try:
+        key = _keys(1, 57)[0]
+        s = b.session_open(key)
+        aes = oracle.Rijndael(key)
+        nthreads, per = 4, 400
+        seen = {t: [] for t in range(nthreads)}
+        outs = {}
+        errs = []
+
+        def worker(t):
+            rng = random.Random(500 + t)
+            for i in range(per):
+                n = 16 * rng.randrange(1, 200)
+                data = bytes(rng.getrandbits(8) for _ in range(n))
+                out = bytearray(n)
+                outs[(t, i)] = (data, out)
+
+                def done(st, t=t, i=i):
+                    if st:
+                        errs.append(st)
+                    if i % 97 == 0:
+                        time.sleep(0.003)  # a slow callback holds up the completion side
+                    seen[t].append(i)
+
+                b.submit(ca.OP_ENCRYPT, s, data, out, None, done)
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert b.flush() == ca.CYAES_OK
+        # flush returned: every callback of the requests above has returned
+        assert all(len(seen[t]) == per for t in range(nthreads))
+        assert not errs
+        for t in range(nthreads):
+            assert seen[t] == list(range(per)), t  # submission order per thread
+        for (t, i), (data, out) in outs.items():
+            assert bytes(out) == bytes(aes.encrypt(bytearray(data)))
+        assert b.stats()["batches"] > 10
+    finally:
+        b.close()
