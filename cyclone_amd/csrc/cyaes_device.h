@@ -334,8 +334,14 @@ __device__ __forceinline__ void prio_feedback(uint32_t* lead, uint32_t step, uin
     else if (d == 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
 }
-constexpr uint32_t kEncPrioDiv = 4;  // steps = 8-block chunks (A/B: 1, 2, 4, 8 -> 4 best)
-constexpr uint32_t kDecPrioDiv = 8;  // steps = 64*kDecRows-block rows (A/B: 4, 8, 16 -> 8)
+#ifndef CYAES_ENC_PRIO_DIV
+#define CYAES_ENC_PRIO_DIV 4
+#endif
+#ifndef CYAES_DEC_PRIO_DIV
+#define CYAES_DEC_PRIO_DIV 8
+#endif
+constexpr uint32_t kEncPrioDiv = CYAES_ENC_PRIO_DIV;  // steps = 8-block chunks (r01 A/B: 1, 2, 4, 8 -> 4 best)
+constexpr uint32_t kDecPrioDiv = CYAES_DEC_PRIO_DIV;  // steps = 64*kDecRows-block rows (r01 A/B: 4, 8, 16 -> 8)
 
 __device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kIv2, kIv3); }
 
