@@ -39,10 +39,20 @@
 //  * Waves of a workgroup are kept level by progress-feedback priority
 //    (prio_feedback), so none runs a starved tail.
 //
+// Translation units (r03), each compiled with the LLVM machine scheduler that
+// measured best for its kernels (Makefile SCHED_*, profiles/r03/ab_sched.txt):
+//   cyaes_kernels.hip      (this file, default scheduler): k_encrypt_quad,
+//                          k_decrypt_ragged, key expansion, workload utilities,
+//                          the debug readers that sum every TU's records;
+//   cyaes_enc_kernels.hip  (iterative ILP): k_encrypt;
+//   cyaes_dec_kernels.hip  (max ILP): k_decrypt_flat, k_boundary_snapshot.
+// Shared device code (access layer, table lookups, rounds, key schedules,
+// priority feedback) is in cyaes_device.h.
+//
 // Build variants (Makefile): CYAES_CLOCK_PROBE (bench.py's in-kernel clock)
 // and CYAES_BOUNDS_CHECK (every global access checked against the extent the
 // batch contract gives it; misses are counted, never faulted).  The rejected
-// A/B variants of rounds 1-2 are recorded in profiles/r0{1,2}/ab_*.txt.
+// A/B variants of rounds 1-3 are recorded in profiles/r0{1,2,3}/ab_*.txt.
 #define CYAES_TU 0
 #include "cyaes_device.h"
 
