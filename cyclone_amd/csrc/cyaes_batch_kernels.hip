@@ -5,8 +5,8 @@
 // Each names its input and output by DEVICE address: host memory the caller
 // registered as a packet pool (hipHostRegister, mapped), or the batcher's own
 // pinned bounce buffer for requests outside every pool.  The GPU moves the
-// bytes itself over PCIe -- one wave per request, 256 B (dwords) or 1 KiB
-// (dwordx4) contiguous per wave instruction -- so the host copies nothing:
+// bytes itself over PCIe -- one wave per request, 1 KiB (dwordx4) contiguous
+// per wave instruction -- so the host copies nothing:
 //   k_batch_gather : input -> the batch's HBM stage, building RELAY_FORWARD
 //                    packets for SEAL on the way (relay_local.cpp:189-201:
 //                    BE u16 size and id, RelayForwardMsg{id, size} in host
@@ -14,8 +14,9 @@
 //                    and writes the ragged kernels' (offset, bytes, key) lists;
 //   (k_encrypt_quad / k_encrypt / k_decrypt_ragged run on the stage in HBM;)
 //   k_batch_scatter: stage -> outputs: the sealed packet (SEAL), the payload
-//                    decrypted in place behind the untouched header (OPEN,
-//                    relay_server.cpp:329), or the CBC output (ENCRYPT/DECRYPT).
+//                    decrypted in place behind its header, whose bytes are
+//                    written back unchanged (OPEN, relay_server.cpp:329), or the
+//                    CBC output (ENCRYPT/DECRYPT).
 #include <algorithm>
 
 #include "cyaes_internal.h"
@@ -29,45 +30,39 @@ constexpr uint32_t kPayload = CYAES_RELAY_PAYLOAD_OFFSET;  // head + RelayForwar
 constexpr uint32_t kForwardId = CYAES_RELAY_FORWARD;       // relay_protocol.h:9-14
 constexpr uint8_t kPad = CYAES_RELAY_PAD;                  // Packet::_resize fill (cye_packet.cpp:102)
 
-// dst[0, n) = src[0, n), one wave: 16 B per lane when both ends and n are
-// 16-B aligned, else dwords when 4-B aligned (the tail bytes singly), else
-// bytes.  Each round issues all its loads before its stores (4 KiB of dwords
-// or 4 KiB of dwordx4 per wave), so a relay packet costs one or two PCIe round
-// trips instead of one per 256 B.
+// 16 B at a 4-byte-aligned address: still one global_load/store_dwordx4.
+struct __attribute__((aligned(4))) Blk4 {
+    uint32_t x, y, z, w;
+};
+
+// dst[0, n) = src[0, n), one wave.  When both ends are 4-B aligned: 16 B per
+// lane (dwordx4 at 4-B alignment), then the last n % 16 bytes as dwords; else
+// bytes.  Each round issues all its loads before its stores (4 KiB per wave),
+// so a relay packet costs one or two PCIe round trips.  The callers place the
+// HBM stage so that the host end of every copy keeps its own alignment (a
+// whole relay packet moves, header included), and only the HBM end of a copy
+// is off 16 B.
 __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t lane) {
     const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
-    if (((a | n) & 15u) == 0) {
-        for (uint32_t o0 = 0; o0 < n; o0 += 4096) {
-            uint4 v[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t o = o0 + 1024 * k + 16 * lane;
-                if (o < n) v[k] = *reinterpret_cast<const uint4*>(src + o);
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t o = o0 + 1024 * k + 16 * lane;
-                if (o < n) *reinterpret_cast<uint4*>(dst + o) = v[k];
-            }
-        }
-        return;
-    }
     uint32_t body = 0;
     if ((a & 3u) == 0) {
-        body = n & ~3u;
+        body = n & ~15u;
         for (uint32_t o0 = 0; o0 < body; o0 += 4096) {
-            uint32_t v[16];
+            Blk4 v[4];
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const uint32_t o = o0 + 256 * k + 4 * lane;
-                if (o < body) v[k] = *reinterpret_cast<const uint32_t*>(src + o);
+            for (int k = 0; k < 4; k++) {
+                const uint32_t o = o0 + 1024 * k + 16 * lane;
+                if (o < body) v[k] = *reinterpret_cast<const Blk4*>(src + o);
             }
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const uint32_t o = o0 + 256 * k + 4 * lane;
-                if (o < body) *reinterpret_cast<uint32_t*>(dst + o) = v[k];
+            for (int k = 0; k < 4; k++) {
+                const uint32_t o = o0 + 1024 * k + 16 * lane;
+                if (o < body) *reinterpret_cast<Blk4*>(dst + o) = v[k];
             }
         }
+        const uint32_t o = body + 4 * lane;  // at most 3 dwords
+        if (o + 4 <= n) *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(src + o);
+        body = n & ~3u;
     }
     for (uint32_t o = body + lane; o < n; o += 64) dst[o] = src[o];
 }
@@ -107,8 +102,9 @@ __device__ __forceinline__ void gather_one(const BatchDesc& d, uint32_t i, uint8
             for (uint32_t o = d.size + lane; o < d.crypt; o += 64) pk[kPayload + o] = kPad;
             break;
         }
-        case kOpRelayOpen:  // the payload only: the header stays where it is
-            wave_copy(s + 16, src + kPayload, d.crypt, lane);
+        case kOpRelayOpen:  // the whole packet at stage + 4 (payload at stage + 16): the host
+                            // end keeps the packet's alignment
+            wave_copy(s + kHead, src, kPayload + d.crypt, lane);
             break;
     }
 }
@@ -124,8 +120,10 @@ __device__ __forceinline__ void scatter_one(const BatchDesc& d, const uint8_t* _
         case kOpRelaySeal:  // the whole packet: header, RelayForwardMsg, ciphertext
             wave_copy(dst, s + kHead, kPayload + d.crypt, lane);
             break;
-        case kOpRelayOpen:  // plaintext back behind the header (in place)
-            wave_copy(dst + kPayload, s + 16, d.crypt, lane);
+        case kOpRelayOpen:  // plaintext back behind the header, in place; the header's 12
+                            // bytes are written back unchanged so that the host end is
+                            // the packet's own alignment (the gather read them)
+            wave_copy(dst, s + kHead, kPayload + d.crypt, lane);
             break;
     }
 }

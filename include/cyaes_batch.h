@@ -35,7 +35,8 @@
  *   SEAL: build the RELAY_FORWARD packet for a chunk (header, RelayForwardMsg,
  *         0xCE padding) and encrypt its payload (relay_local.cpp:189-206);
  *   OPEN: decrypt a received RELAY_FORWARD packet's payload in place
- *         (relay_server.cpp:329).
+ *         (relay_server.cpp:329); the whole packet is read and written back,
+ *         its 12 header bytes unchanged.
  *
  * Pipelining: `inflight` stages; while the GPU runs batch k the builder lays
  * out batch k+1 and the completion side runs k-1's callbacks.  Callbacks run
