@@ -120,7 +120,9 @@ def live_traffic(timeout_s=150):
     with tempfile.TemporaryDirectory(prefix="cyaes_pmc_") as tmp:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, counter)
-            cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+            # rocprofv3 is a python script: run it with this interpreter, so the
+            # only exec is rocprofv3's own of the profiled program
+            cmd = [sys.executable, prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
                    sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C", "--steps", "2", "--warmup", "0",
                    "--no-cpu", "--no-verify", "--no-clock", "--packet-configs", "none", "--relay-stream", "0",
                    "--traffic", "none"]
@@ -221,12 +223,23 @@ def cpu_baseline(cfg_name, npay, pb, ppk, d_ct, torch, sample=0):
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # The traffic passes run first, before this process touches the GPU: each
+    # is a child process (rocprofv3 starts the profiled bench.py by exec), and
+    # no process that has initialised the GPU may be the parent of an exec chain.
+    live, why = (None, "not requested")
+    under_prof = any(k.startswith("ROCPROF_") for k in os.environ)  # this run is itself being profiled
+    if args.traffic == "live" and rank == 0 and world == 1 and args.config in ("C", "E"):
+        if under_prof:
+            why = "running under rocprofv3: no nested profiler passes"
+        else:
+            log("hbm traffic: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (config C) ...")
+            live, why = live_traffic()
+    import torch
+    import torch.distributed as dist
+
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     # Rehearsal knobs for a 1-GPU box (never used by the driver): run every rank
@@ -524,10 +537,6 @@ def main():
     ftr = None
     if os.path.exists(tfile):
         ftr = json.load(open(tfile)).get("C" if args.config == "E" else args.config, {}).get(dom)
-    live, why = (None, "not requested")
-    if args.traffic == "live" and rank == 0 and world == 1 and args.config in ("C", "E"):
-        log("hbm traffic: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (config C) ...")
-        live, why = live_traffic()
     if live and dom in live:
         algo = 2.0 * nbytes
         roofline["traffic"] = live[dom]

@@ -47,11 +47,11 @@ for step in "$@"; do
     quickbench) run quickbench 300 python bench.py --steps 3 --warmup 1 --no-cpu ;;
     profile)
       (cd /tmp && run rocprof_stats 300 rocprofv3 --kernel-trace --stats -d "$O/rocprof" -o run --output-format csv \
-        -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --packet-configs none --relay-stream 0) || exit $?
+        -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --packet-configs none --relay-stream 0 --traffic none) || exit $?
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && run pmc_$c 300 rocprofv3 --pmc $c -d "$O/pmc_$c" -o run --output-format csv \
           -- python3 "$R/bench.py" --config C --steps 2 --warmup 0 --no-cpu --no-verify --no-clock \
-             --packet-configs none --relay-stream 0) || exit $?
+             --packet-configs none --relay-stream 0 --traffic none) || exit $?
       done ;;
     batchertest) run pytest_batcher 300 python -u -m pytest tests/test_batcher.py -m gpu -x -v --timeout 150 --timeout-method thread ;;
     batcher)  # SEAL / OPEN host to host: zero-copy pools (pointer and offset submits), then the bounce path
