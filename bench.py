@@ -100,6 +100,19 @@ def parse():
     return ap.parse_args()
 
 
+def traffic_plan(traffic, rank, world, config, environ):
+    """(run the live traffic passes?, reason if not): rank 0 at N = 1 on the
+    config C / E kernels, and never when this bench.py is itself being profiled
+    (rocprofv3 sets ROCPROF_* for the program it runs): no nested passes."""
+    if traffic != "live":
+        return False, "not requested"
+    if rank != 0 or world != 1 or config not in ("C", "E"):
+        return False, "rank 0 at N = 1 on config C / E only"
+    if any(k.startswith("ROCPROF_") for k in environ):
+        return False, "running under rocprofv3: no nested profiler passes"
+    return True, None
+
+
 def live_traffic(timeout_s=150):
     """HBM bytes per AES launch, measured now: two rocprofv3 --pmc passes
     (FETCH_SIZE, WRITE_SIZE; one counter each, as MI355X_MICROARCH.md's
@@ -230,13 +243,10 @@ def main():
     # is a child process (rocprofv3 starts the profiled bench.py by exec), and
     # no process that has initialised the GPU may be the parent of an exec chain.
     live, why = (None, "not requested")
-    under_prof = any(k.startswith("ROCPROF_") for k in os.environ)  # this run is itself being profiled
-    if args.traffic == "live" and rank == 0 and world == 1 and args.config in ("C", "E"):
-        if under_prof:
-            why = "running under rocprofv3: no nested profiler passes"
-        else:
-            log("hbm traffic: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (config C) ...")
-            live, why = live_traffic()
+    run_passes, why = traffic_plan(args.traffic, rank, world, args.config, os.environ)
+    if run_passes:
+        log("hbm traffic: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (config C) ...")
+        live, why = live_traffic()
     import torch
     import torch.distributed as dist
 

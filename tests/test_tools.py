@@ -62,3 +62,40 @@ def test_traffic_json_corrections(tmp_path):
         assert t[k]["bytes_per_launch"] == traffic.ALGO
         assert t[k]["ratio"] == 1.0
         assert t[k]["fetch_bytes"] == traffic.ALGO // 2
+
+
+def test_bench_traffic_plan_and_pass_command(monkeypatch):
+    """bench.py's live HBM-traffic passes: only rank 0 at N = 1 on config C / E,
+    never nested under rocprofv3, and each pass is the rocprofv3 script run by
+    this interpreter (no exec hop through `env`) over a bench.py that runs no
+    passes of its own."""
+    import shutil
+    import subprocess
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.traffic_plan("live", 0, 1, "E", {}) == (True, None)
+    assert bench.traffic_plan("live", 0, 1, "C", {"PATH": "/bin"})[0] is True
+    assert bench.traffic_plan("file", 0, 1, "E", {})[0] is False
+    assert bench.traffic_plan("live", 1, 2, "E", {})[0] is False
+    assert bench.traffic_plan("live", 0, 1, "B", {})[0] is False
+    run, why = bench.traffic_plan("live", 0, 1, "E", {"ROCPROF_COUNTER_COLLECTION": "1"})
+    assert run is False and "rocprofv3" in why
+    if not shutil.which("rocprofv3"):
+        pytest.skip("rocprofv3 not on PATH")
+    seen = []
+
+    class Fake:
+        returncode = 3
+
+        def __init__(self, cmd, **kw):
+            seen.append((cmd, kw))
+
+        def wait(self, timeout=None):
+            return self.returncode
+    monkeypatch.setattr(subprocess, "Popen", Fake)
+    live, why = bench.live_traffic(timeout_s=5)
+    assert live is None and "exited 3" in why
+    cmd, kw = seen[0]
+    assert cmd[0] == sys.executable and cmd[1].endswith("rocprofv3") and cmd[2:4] == ["--pmc", "FETCH_SIZE"]
+    assert cmd[cmd.index("--") + 1] == sys.executable
+    assert cmd[-2:] == ["--traffic", "none"] and "RANK" not in kw["env"] and kw["start_new_session"]
