@@ -46,7 +46,7 @@ BOBJ     := $(BUILD)/cyaes_batch_kernels.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
 .PHONY: all lib mgpu oracle cpptest probe bounds microbench variant clean
-all: lib mgpu oracle cpptest probe bounds $(BUILD)/bench_batcher $(BUILD)/dropin_threads $(BUILD)/bitslice $(BUILD)/hostlink
+all: lib mgpu oracle cpptest probe bounds $(BUILD)/bench_batcher $(BUILD)/relay_loop $(BUILD)/dropin_threads $(BUILD)/bitslice $(BUILD)/hostlink
 lib: $(LIB)
 mgpu: $(MGPU)
 oracle: $(ORACLE)
@@ -133,3 +133,7 @@ variant: $(HOBJ) $(AOBJ) $(BOBJ) | $(BUILD)
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(MGPU) $(ORACLE)
+
+# The relay's whole data path through the batching adapter (SEAL, tunnel stream, parse, OPEN), one process
+$(BUILD)/relay_loop: tools/relay_loop.cpp $(LIB) $(HDRS) | $(BUILD)
+	$(CXX) -O2 -std=c++17 -Wall -pthread $(INC) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'

@@ -4,6 +4,7 @@ checked against the AES oracle and the relay restatement
 (oracle/relay_oracle.py).  Each request must equal the reference's
 synchronous Rijndael call with iv = nullptr (relay_local.cpp:206,365;
 relay_server.cpp:329,472)."""
+import os
 import random
 import struct
 import threading
@@ -671,3 +672,27 @@ def test_slow_callbacks_keep_order_and_flush_semantics():
         assert b.stats()["batches"] > 10
     finally:
         b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,recv_copy", [("1472", 1), ("rand:4000", 0), ("rand:65280", 1)])
+def test_relay_loop_both_ends(size, recv_copy):
+    """tools/relay_loop: the relay's whole data path through the batcher --
+    SEAL chunks into per-pipe tunnel streams (packets back to back, as TCP
+    carries them; relay_local.cpp:188-217), cut the received stream into
+    packets (cye_packet.cpp:166-181), OPEN each in place (relay_server.cpp:329)
+    -- and every forwarded payload, RelayForwardMsg field and 0xCE pad byte
+    matches the client's chunk; the wire holds ciphertext."""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "build", "relay_loop")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", root, "-s", "build/relay_loop"], check=True)
+    cmd = [exe, "--threads", "3", "--pipes", "4", "--chunks", "8" if size == "rand:65280" else "32",
+           "--size", size, "--recv-copy", str(recv_copy), "--seconds", "0.3"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["error"] == 0 and out["mismatches"] == 0
+    assert out["verified"] == out["packets"] > 0 and out["rounds"] > 0
