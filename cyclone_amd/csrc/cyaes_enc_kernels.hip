@@ -5,10 +5,43 @@
 // cyaes_kernels.hip and DESIGN.md §3.2.
 
 #define CYAES_TU 1
+#include <type_traits>
+
 #include "cyaes_device.h"
 
 namespace cyaes {
 namespace {
+
+#ifndef CYAES_ENC_COAL
+#define CYAES_ENC_COAL 1
+#endif
+
+// 4x4 transpose of 16-B blocks among the lanes k, k+16, k+32, k+48 (rows of
+// the wave, "members" m = lane >> 4): member m's r[t] becomes member t's r[m].
+// Two butterfly stages, one v_permlane16_swap / v_permlane32_swap per dword
+// and register pair (gfx950), in place.
+__device__ __forceinline__ void swap16(uint32_t& x, uint32_t& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+}
+__device__ __forceinline__ void swap32(uint32_t& x, uint32_t& y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+}
+__device__ __forceinline__ void swap16(uint4& a, uint4& b) {
+    swap16(a.x, b.x), swap16(a.y, b.y), swap16(a.z, b.z), swap16(a.w, b.w);
+}
+__device__ __forceinline__ void swap32(uint4& a, uint4& b) {
+    swap32(a.x, b.x), swap32(a.y, b.y), swap32(a.z, b.z), swap32(a.w, b.w);
+}
+__device__ __forceinline__ void transpose4(uint4* r) {
+    swap16(r[0], r[1]);
+    swap16(r[2], r[3]);
+    swap32(r[0], r[2]);
+    swap32(r[1], r[3]);
+}
 
 // ---- CBC encrypt: one lane per payload chain (cyr_rijndael.cpp:588-609) ----
 // RUNS (uniform batches of short payloads, no IV arrays): a lane's work item
@@ -70,6 +103,14 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
         }
         // RUNS + KEYED: the runtime makes runs divide payloads_per_key, so the run is one session
         const uint32_t kid = KEYED ? key_index(a.keys, p, a.npayloads, active, a.status) : 0u;
+        // Coalesced chunk moves (uniform batches without per-lane keys, full waves
+        // of equal work items): load / store j of a chunk moves 64 contiguous bytes
+        // of one work item with the 4 lanes k, k+16, k+32, k+48, and the blocks
+        // reach their own lanes by transpose4.  A wave instruction then touches
+        // 16 half-lines instead of 64 lines, which the power-limited clock repays
+        // (cost probe: encrypt -4 %, profiles/r03/probe_coalesced_clock.txt).
+        const bool coal = CYAES_ENC_COAL && !RAGGED && !KEYED && a.iv_in == nullptr &&
+                          __ballot(active && nb == __builtin_amdgcn_readfirstlane(nb)) == ~0ull;
         bool pending = active;
         while (true) {  // waterfall over the distinct keys of this wave
             const uint64_t m = __ballot(pending);
@@ -84,72 +125,110 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                 const Ext se = ext(src, 16ull * nb), de = ext(dst, 16ull * nb);  // this work item's bytes
                 uint32_t nr = bpp;  // RUNS: block index of the next chain restart (a payload start)
                 uint32_t i = 0;
-                uint4 b[8];
-                if (nb >= 8) {
+                // coal: member 0's work item of this lane's group, and the bytes between members
+                const uint32_t mem = lane >> 4;
+                const uint64_t mstride = 16ull * R * a.payload_bytes;
+                const uint8_t* gsrc = src - mem * mstride;
+                uint8_t* gdst = dst - mem * mstride;
+                const Ext ge = ext(a.in, (uint64_t)a.npayloads * a.payload_bytes);
+                const Ext gde = ext(a.out, (uint64_t)a.npayloads * a.payload_bytes);
+                // 8 blocks from block kk of this lane's work item into v[0..7]; coal:
+                // still transposed (the caller transposes once the loads have landed,
+                // so a prefetch stays in flight during the chunk's rounds)
+                auto load8 = [&](auto co_tag, uint4 (&v)[8], uint32_t kk) {
+                    if constexpr (decltype(co_tag)::value) {
+                        const uint8_t* q = gsrc + 16ull * (kk + mem);
 #pragma unroll
-                    for (int j = 0; j < 8; j++) b[j] = ldb<RAGGED>(src, j, se);
-                }
-                bool have_tail = false;  // b[8 - (nb - i), 8) already hold the last partial chunk
-                for (; i + 8 <= nb; i += 8) {
-                    const bool more = i + 16 <= nb;
-                    const bool tail = !more && i + 8 < nb;  // partial last chunk
-                    // Next chunk's loads in flight during this chunk's rounds (-8 %
-                    // encrypt time).  One set of 8 loads for both cases: a partial
-                    // last chunk loads the payload's last 8 blocks (its tail then
-                    // sits at the top of bn).  With every bn[j] defined on this
-                    // path the compiler no longer waits for this chunk's stores
-                    // (s_waitcnt vmcnt(0)) before the next chunk's loads; it waits
-                    // only for the loads (profiles/r02/ab_onepf.txt).
-                    uint4 bn[8];
-                    if (more || tail) {
-                        const uint8_t* nsrc = src + 16ull * (more ? i + 8 : nb - 8);
+                        for (int j = 0; j < 8; j++) v[j] = LD16(q + (j & 3) * mstride + 64 * (j >> 2), ge);
+                    } else {
+                        const uint8_t* q = src + 16ull * kk;
 #pragma unroll
-                        for (int j = 0; j < 8; j++) bn[j] = ldb<RAGGED>(nsrc, j, se);
+                        for (int j = 0; j < 8; j++) v[j] = ldb<RAGGED>(q, j, se);
                     }
-                    prio_feedback(&lead, ++prog, kEncPrioDiv);
+                };
+                // The chunk loop, with the coalesced moves compiled in or out (one
+                // branch per work item: inside the loop a join of the two store paths
+                // made the compiler drain every store before the next loads).
+                auto chunks = [&](auto co_tag) {
+                    constexpr bool CO = decltype(co_tag)::value;
+                    uint4 b[8];
+                    if (nb >= 8) {
+                        load8(co_tag, b, 0);
+                        if constexpr (CO) transpose4(b), transpose4(b + 4);
+                    }
+                    bool have_tail = false;  // b[8 - (nb - i), 8) already hold the last partial chunk
+                    for (; i + 8 <= nb; i += 8) {
+                        const bool more = i + 16 <= nb;
+                        const bool tail = !more && i + 8 < nb;  // partial last chunk
+                        // Next chunk's loads in flight during this chunk's rounds (-8 %
+                        // encrypt time).  One set of 8 loads for both cases: a partial
+                        // last chunk loads the payload's last 8 blocks (its tail then
+                        // sits at the top of bn).  With every bn[j] defined on this
+                        // path the compiler no longer waits for this chunk's stores
+                        // (s_waitcnt vmcnt(0)) before the next chunk's loads; it waits
+                        // only for the loads (profiles/r02/ab_onepf.txt).
+                        uint4 bn[8];
+                        if (more || tail) load8(co_tag, bn, more ? i + 8 : nb - 8);
+                        prio_feedback(&lead, ++prog, kEncPrioDiv);
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        if (RUNS && i + j == nr) {  // next payload of the run: a new chain
+                        for (int j = 0; j < 8; j++) {
+                            if (RUNS && i + j == nr) {  // next payload of the run: a new chain
+                                c = default_iv();
+                                nr += bpp;
+                            }
+                            uint32_t s0 = xor3(c.x, b[j].x, ek[0]), s1 = xor3(c.y, b[j].y, ek[1]);
+                            uint32_t s2 = xor3(c.z, b[j].z, ek[2]), s3 = xor3(c.w, b[j].w, ek[3]);
+                            enc_block(lds, lo, ek, s0, s1, s2, s3);
+                            c = make_uint4(s0, s1, s2, s3);
+                            b[j] = c;
+                        }
+                        if constexpr (CO) {  // the transposes back, then 64 contiguous bytes of one work item per store
+                            transpose4(b);
+                            transpose4(b + 4);
+                            uint8_t* const q = gdst + 16ull * (i + mem);
+#pragma unroll
+                            for (int j = 0; j < 8; j++) ST16(q + (j & 3) * mstride + 64 * (j >> 2), gde, b[j]);
+                        } else {
+                            uint8_t* const dchunk = dst + 16ull * i;  // one address, immediate offsets (ragged too)
+#pragma unroll
+                            for (int j = 0; j < 8; j++) stb<RAGGED>(dchunk, j, b[j], de);  // (nt stores measured 3.6x slower)
+                        }
+                        if (more || tail) {
+#pragma unroll
+                            for (int j = 0; j < 8; j++) b[j] = bn[j];
+                            if constexpr (CO) transpose4(b), transpose4(b + 4);
+                        }
+                        have_tail = tail;
+                    }
+                    if (have_tail) {  // the tail's nb - i blocks sit in b[8 - (nb - i), 8): move them down to b[0]
+#pragma unroll
+                        for (int sft = 1; sft < 8; sft++) {
+                            if (sft <= 8 - (int)(nb - i)) {
+#pragma unroll
+                                for (int j = 0; j < 7; j++) b[j] = b[j + 1];
+                            }
+                        }
+                    }
+                    for (; i < nb; i++) {  // partial last chunk: from b (prefetched) or loaded here
+                        const uint4 v = have_tail ? b[0] : ldb<RAGGED>(src, i, se);
+#pragma unroll
+                        for (int j = 0; j < 7; j++) b[j] = b[j + 1];
+                        if (RUNS && i == nr) {
                             c = default_iv();
                             nr += bpp;
                         }
-                        uint32_t s0 = xor3(c.x, b[j].x, ek[0]), s1 = xor3(c.y, b[j].y, ek[1]);
-                        uint32_t s2 = xor3(c.z, b[j].z, ek[2]), s3 = xor3(c.w, b[j].w, ek[3]);
+                        uint32_t s0 = xor3(c.x, v.x, ek[0]), s1 = xor3(c.y, v.y, ek[1]);
+                        uint32_t s2 = xor3(c.z, v.z, ek[2]), s3 = xor3(c.w, v.w, ek[3]);
                         enc_block(lds, lo, ek, s0, s1, s2, s3);
                         c = make_uint4(s0, s1, s2, s3);
-                        b[j] = c;
+                        stb<RAGGED>(dst, i, c, de);
                     }
-                    uint8_t* const dchunk = dst + 16ull * i;  // one address, immediate offsets (ragged too)
-#pragma unroll
-                    for (int j = 0; j < 8; j++) stb<RAGGED>(dchunk, j, b[j], de);  // (nt stores measured 3.6x slower)
-                    if (more || tail) {
-#pragma unroll
-                        for (int j = 0; j < 8; j++) b[j] = bn[j];
-                    }
-                    have_tail = tail;
-                }
-                if (have_tail) {  // the tail's nb - i blocks sit in b[8 - (nb - i), 8): move them down to b[0]
-#pragma unroll
-                    for (int sft = 1; sft < 8; sft++) {
-                        if (sft <= 8 - (int)(nb - i)) {
-#pragma unroll
-                            for (int j = 0; j < 7; j++) b[j] = b[j + 1];
-                        }
-                    }
-                }
-                for (; i < nb; i++) {  // partial last chunk: from b (prefetched) or loaded here
-                    const uint4 v = have_tail ? b[0] : ldb<RAGGED>(src, i, se);
-#pragma unroll
-                    for (int j = 0; j < 7; j++) b[j] = b[j + 1];
-                    if (RUNS && i == nr) {
-                        c = default_iv();
-                        nr += bpp;
-                    }
-                    uint32_t s0 = xor3(c.x, v.x, ek[0]), s1 = xor3(c.y, v.y, ek[1]);
-                    uint32_t s2 = xor3(c.z, v.z, ek[2]), s3 = xor3(c.w, v.w, ek[3]);
-                    enc_block(lds, lo, ek, s0, s1, s2, s3);
-                    c = make_uint4(s0, s1, s2, s3);
-                    stb<RAGGED>(dst, i, c, de);
+                };
+                if constexpr (!RAGGED && !KEYED) {
+                    if (coal) chunks(std::true_type{});
+                    else chunks(std::false_type{});
+                } else {
+                    chunks(std::false_type{});
                 }
                 if (a.iv_out) ST16(a.iv_out + 16 * p, iv_out_e, c);  // (RUNS: no IV arrays)
             }
