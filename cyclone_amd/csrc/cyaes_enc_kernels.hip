@@ -15,6 +15,9 @@ namespace {
 #ifndef CYAES_ENC_COAL
 #define CYAES_ENC_COAL 1
 #endif
+#ifndef CYAES_ENC_COAL_RAGGED
+#define CYAES_ENC_COAL_RAGGED 1
+#endif
 
 // 4x4 transpose of 16-B blocks among the lanes k, k+16, k+32, k+48 (rows of
 // the wave, "members" m = lane >> 4): member m's r[t] becomes member t's r[m].
@@ -103,14 +106,18 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
         }
         // RUNS + KEYED: the runtime makes runs divide payloads_per_key, so the run is one session
         const uint32_t kid = KEYED ? key_index(a.keys, p, a.npayloads, active, a.status) : 0u;
-        // Coalesced chunk moves (uniform batches without per-lane keys, full waves
-        // of equal work items): load / store j of a chunk moves 64 contiguous bytes
-        // of one work item with the 4 lanes k, k+16, k+32, k+48, and the blocks
-        // reach their own lanes by transpose4.  A wave instruction then touches
-        // 16 half-lines instead of 64 lines, which the power-limited clock repays
-        // (cost probe: encrypt -4 %, profiles/r03/probe_coalesced_clock.txt).
-        const bool coal = CYAES_ENC_COAL && !RAGGED && !KEYED && a.iv_in == nullptr &&
-                          __ballot(active && nb == __builtin_amdgcn_readfirstlane(nb)) == ~0ull;
+        // Coalesced chunk moves (batches without per-lane keys or IV arrays, full
+        // waves of equal work items; ragged batches only in place): load / store j
+        // of a chunk moves 64 contiguous bytes of one work item with the 4 lanes
+        // k, k+16, k+32, k+48, and the blocks reach their own lanes by transpose4.
+        // A wave instruction then touches 16 half-lines instead of 64 lines, which
+        // the power-limited clock repays (config C encrypt -2 %), and a relay
+        // stream's misaligned payloads are stored 64 contiguous bytes at a time
+        // (1 M relay packets in place -6 %; out of place it measured +3 %, so
+        // out-of-place ragged batches keep the per-lane moves;
+        // profiles/r03/ab_enc_coalesced.txt).
+        const bool coal = CYAES_ENC_COAL && (!RAGGED || (CYAES_ENC_COAL_RAGGED && a.in == a.out)) && !KEYED &&
+                          a.iv_in == nullptr && __ballot(active && nb == __builtin_amdgcn_readfirstlane(nb)) == ~0ull;
         bool pending = active;
         while (true) {  // waterfall over the distinct keys of this wave
             const uint64_t m = __ballot(pending);
@@ -132,11 +139,28 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                 uint8_t* gdst = dst - mem * mstride;
                 const Ext ge = ext(a.in, (uint64_t)a.npayloads * a.payload_bytes);
                 const Ext gde = ext(a.out, (uint64_t)a.npayloads * a.payload_bytes);
+                uint64_t moff[4] = {0, 0, 0, 0};  // ragged coal: byte offsets of the group's work items
+                if constexpr (RAGGED) {
+                    if (coal) {
+#pragma unroll
+                        for (int t = 0; t < 4; t++) {
+                            const int from = (int)((lane & 15u) + 16u * t);
+                            moff[t] = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), from) << 32 |
+                                      (uint32_t)__shfl((int)(uint32_t)off, from);
+                        }
+                    }
+                }
                 // 8 blocks from block kk of this lane's work item into v[0..7]; coal:
                 // still transposed (the caller transposes once the loads have landed,
                 // so a prefetch stays in flight during the chunk's rounds)
                 auto load8 = [&](auto co_tag, uint4 (&v)[8], uint32_t kk) {
-                    if constexpr (decltype(co_tag)::value) {
+                    if constexpr (decltype(co_tag)::value && RAGGED) {
+#pragma unroll
+                        for (int j = 0; j < 8; j++) {
+                            const uint8_t* w0 = a.in + moff[j & 3];
+                            v[j] = LD16U(w0 + 16ull * (kk + 4 * (j >> 2) + mem), ext(w0, 16ull * nb));
+                        }
+                    } else if constexpr (decltype(co_tag)::value) {
                         const uint8_t* q = gsrc + 16ull * (kk + mem);
 #pragma unroll
                         for (int j = 0; j < 8; j++) v[j] = LD16(q + (j & 3) * mstride + 64 * (j >> 2), ge);
@@ -185,9 +209,17 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                         if constexpr (CO) {  // the transposes back, then 64 contiguous bytes of one work item per store
                             transpose4(b);
                             transpose4(b + 4);
-                            uint8_t* const q = gdst + 16ull * (i + mem);
+                            if constexpr (RAGGED) {
 #pragma unroll
-                            for (int j = 0; j < 8; j++) ST16(q + (j & 3) * mstride + 64 * (j >> 2), gde, b[j]);
+                                for (int j = 0; j < 8; j++) {
+                                    uint8_t* w0 = a.out + moff[j & 3];
+                                    ST16U(w0 + 16ull * (i + 4 * (j >> 2) + mem), ext(w0, 16ull * nb), b[j]);
+                                }
+                            } else {
+                                uint8_t* const q = gdst + 16ull * (i + mem);
+#pragma unroll
+                                for (int j = 0; j < 8; j++) ST16(q + (j & 3) * mstride + 64 * (j >> 2), gde, b[j]);
+                            }
                         } else {
                             uint8_t* const dchunk = dst + 16ull * i;  // one address, immediate offsets (ragged too)
 #pragma unroll
@@ -224,7 +256,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
                         stb<RAGGED>(dst, i, c, de);
                     }
                 };
-                if constexpr (!RAGGED && !KEYED) {
+                if constexpr (!KEYED && (!RAGGED || CYAES_ENC_COAL_RAGGED)) {
                     if (coal) chunks(std::true_type{});
                     else chunks(std::false_type{});
                 } else {
