@@ -335,12 +335,16 @@ __device__ __forceinline__ void prio_feedback(uint32_t* lead, uint32_t step, uin
     else __builtin_amdgcn_s_setprio(0);
 }
 #ifndef CYAES_ENC_PRIO_DIV
-#define CYAES_ENC_PRIO_DIV 4
+#define CYAES_ENC_PRIO_DIV 1
 #endif
 #ifndef CYAES_DEC_PRIO_DIV
 #define CYAES_DEC_PRIO_DIV 8
 #endif
-constexpr uint32_t kEncPrioDiv = CYAES_ENC_PRIO_DIV;  // steps = 8-block chunks (r01 A/B: 1, 2, 4, 8 -> 4 best)
+// steps = 8-block chunks.  r01 A/B on config C: 1, 2, 4, 8 -> 4 best; r03 (after the
+// runs and the coalesced moves): 1 -> configs B / D / relay stream -4.5 to -4.8 %
+// (their ~1 ms launches end with a 12 % wave spread at 4), config C unchanged
+// (profiles/r03/ab_prio_div_s2.txt).
+constexpr uint32_t kEncPrioDiv = CYAES_ENC_PRIO_DIV;
 constexpr uint32_t kDecPrioDiv = CYAES_DEC_PRIO_DIV;  // steps = 64*kDecRows-block rows (r01 A/B: 4, 8, 16 -> 8)
 
 __device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kIv2, kIv3); }
