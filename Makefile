@@ -46,7 +46,7 @@ BOBJ     := $(BUILD)/cyaes_batch_kernels.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
 
 .PHONY: all lib mgpu oracle cpptest probe bounds microbench variant clean
-all: lib mgpu oracle cpptest probe bounds $(BUILD)/bench_batcher $(BUILD)/relay_loop $(BUILD)/dropin_threads $(BUILD)/bitslice $(BUILD)/hostlink
+all: lib mgpu oracle cpptest probe bounds $(BUILD)/bench_batcher $(BUILD)/relay_loop $(BUILD)/dropin_threads $(BUILD)/hostlink
 lib: $(LIB)
 mgpu: $(MGPU)
 oracle: $(ORACLE)
@@ -122,10 +122,6 @@ $(PROBE): $(KSRC) $(ESRC) $(DSRC) $(KHDRS) $(HOBJ) $(AOBJ) $(BOBJ)
 
 $(BOUNDS): $(KSRC) $(ESRC) $(DSRC) $(KHDRS) $(HOBJ) $(AOBJ) $(BOBJ)
 	$(call kvariant,bounds,-DCYAES_BOUNDS_CHECK=1)
-
-# Bitsliced decrypt prototype (measurement tool)
-$(BUILD)/bitslice: tools/bitslice.hip tools/bitslice_gen.h $(LIB) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -o $@ $< -Lcyclone_amd -lcyaes -Wl,-rpath,'$$ORIGIN/../cyclone_amd'
 
 # A/B variants: make variant NAME=x DEFS="-DFOO=1" -> build/variants/x.so
 variant: $(HOBJ) $(AOBJ) $(BOBJ) | $(BUILD)

@@ -1,6 +1,6 @@
 // tools/vbank.hip -- does v_bitop3_b32 issue slower when its three VGPR
 // sources share a register bank (VGPR index mod 4)?  The bitsliced decrypt
-// prototype (tools/bitslice.hip) issues ~51 lane-ops/clk/CU where a
+// prototype (tools/bitslice.hip, removed in r04; git history) issues ~51 lane-ops/clk/CU where a
 // v_bitop3_b32 microbench (tools/valurate.hip, sources in distinct banks)
 // reached ~100.  Explicit VGPR numbers, 8 independent chains per wave,
 // 16 waves/CU, in-kernel clock.
