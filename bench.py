@@ -94,6 +94,9 @@ def parse():
     ap.add_argument("--traffic", default="live", choices=["live", "file", "none"],
                     help="roofline.traffic: live = rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over config C "
                          "run as child processes in this run (rank 0, N=1); file = profiles/traffic.json")
+    ap.add_argument("--e2e-gib", type=int, default=8,
+                    help="rank 0 at N = 1, config E/C: GiB of 64 KiB payloads in pinned host memory streamed "
+                         "H2D -> encrypt -> decrypt -> D2H for the `e2e` object (0 = skip)")
     ap.add_argument("--packet-warmup", type=int, default=20,
                     help="untimed steps before each packet config (a 1,472-B step is ~2 ms; 20 cover the clock "
                          "ramp, profiles/r01/packet_warmup.txt)")
@@ -138,7 +141,7 @@ def live_traffic(timeout_s=150):
             cmd = [sys.executable, prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
                    sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C", "--steps", "2", "--warmup", "0",
                    "--no-cpu", "--no-verify", "--no-clock", "--packet-configs", "none", "--relay-stream", "0",
-                   "--traffic", "none"]
+                   "--e2e-gib", "0", "--traffic", "none"]
             env = dict(os.environ)
             for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
                 env.pop(k, None)
@@ -234,9 +237,142 @@ def cpu_baseline(cfg_name, npay, pb, ppk, d_ct, torch, sample=0):
     }, **facts)
 
 
+LAUNCH_ENV = "CYAES_BENCH_LAUNCHER"          # set by the parent for the ranks it starts
+TRAFFIC_ENV = "CYAES_BENCH_LIVE_TRAFFIC"     # the parent's live traffic result, JSON, for rank 0
+
+
+def world_check(gpus, environ):
+    """(world size, error): the ranks this process belongs to.  Under torchrun
+    WORLD_SIZE must equal --gpus; without it the process is rank 0 of 1 (and
+    for --gpus N > 1 it becomes the launcher of N ranks, see launcher_cmd)."""
+    w = environ.get("WORLD_SIZE")
+    if w is None:
+        return 1, None
+    if int(w) != gpus:
+        return int(w), ("--gpus %d but WORLD_SIZE %s: refusing to time a different number of GPUs than "
+                        "asked for" % (gpus, w))
+    return int(w), None
+
+
+def free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launcher_cmd(gpus, argv, port, python=sys.executable):
+    """The child command `python bench.py --gpus N ...` runs when it is not
+    already a torchrun rank: one process per GPU on this node, rendezvous on
+    127.0.0.1, the same bench.py arguments."""
+    return [python, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py")] + list(argv)
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 without torchrun (the driver's `python3 bench.py --gpus N`):
+    this process never touches the GPU.  It runs the live HBM-traffic passes
+    first (child processes, one GPU), then starts torchrun with N ranks as a
+    child process, hands the traffic result to rank 0 through the environment,
+    forwards rank 0's JSON line (adding `launcher`) and exits with the child's
+    return code."""
+    import signal
+    import subprocess
+    env = dict(os.environ)
+    run_passes, why = traffic_plan(args.traffic, 0, 1, args.config, os.environ)
+    live = None
+    if run_passes:
+        log("hbm traffic: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (config C, one GPU) ...")
+        live, why = live_traffic()
+    env[TRAFFIC_ENV] = json.dumps({"traffic": live, "why": why})
+    env[LAUNCH_ENV] = "bench.py"
+    cmd = launcher_cmd(args.gpus, argv, free_port())
+    log("launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    proc = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True)
+
+    def stop(signum, _frame):
+        try:
+            os.killpg(proc.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            pass
+        raise SystemExit(128 + signum)
+    old = {sig: signal.signal(sig, stop) for sig in (signal.SIGTERM, signal.SIGINT)}
+    lines = 0
+    for line in proc.stdout:
+        text = line.strip()
+        if text.startswith("{"):
+            try:
+                out = json.loads(text)
+            except ValueError:
+                out = None
+            if isinstance(out, dict) and out.get("metric") == METRIC:
+                out["launcher"] = {"kind": "bench.py -> torch.distributed.run child", "nproc_per_node": args.gpus}
+                print(json.dumps(out), flush=True)
+                lines += 1
+                continue
+        sys.stderr.write(line)
+        sys.stderr.flush()
+    rc = proc.wait()
+    for sig, h in old.items():
+        signal.signal(sig, h)
+    if rc == 0 and lines != 1:
+        log("error: the ranks exited 0 but printed %d result lines" % lines)
+        rc = 1
+    return rc
+
+
+def run_e2e(ctx, torch, d_pt, d_ct, npay, pb, gib_cap, chunk=256 << 20):
+    """`e2e` object: n = min(gib_cap GiB, this pass) payloads of pb bytes in
+    pinned host memory (torch pin_memory = hipHostMalloc), streamed through
+    cyaes_gpu_encrypt_host and cyaes_gpu_decrypt_host (H2D -> AES -> D2H on a
+    ring of three device slot pairs), best of 3 after one untimed
+    call; beside it the pinned copy ceilings of this box, measured in the same
+    run (tools/linkprobe.py).  bit_exact: the host ciphertext equals the
+    device-resident ciphertext of the same payloads (pass 0, checked against its
+    OpenSSL digest earlier in this run) and the round trip restores the
+    plaintext."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_e2e
+    import linkprobe
+    n = min(npay, max(1, (gib_cap << 30) // pb))
+    nb = n * pb
+    h_pt = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    h_ct = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    h_rt = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    h_pt.copy_(d_pt[:nb])
+    t_e, t_d, ok = bench_e2e.measure(ctx, h_pt, h_ct, h_rt, n, pb, chunk, 3)
+    piece = 1 << 30
+    tmp = torch.empty(min(nb, piece), dtype=torch.uint8, device="cuda")
+    for o in range(0, nb, piece):
+        m = min(piece, nb - o)
+        tmp[:m].copy_(h_ct[o:o + m])
+        ok = ok and bool(torch.equal(tmp[:m], d_ct[o:o + m]))
+    torch.cuda.synchronize()
+    del tmp, h_pt, h_ct, h_rt
+    link = linkprobe.measure(torch, min(nb, 4 << 30), chunk, 3)
+    gib = float(1 << 30)
+    encdec = 2 * nb / (t_e + t_d) / gib
+    return {
+        "unit": "GiB/s", "payloads": n, "payload_bytes": pb, "bytes": nb, "host_memory": "pinned",
+        "path": "cyaes_gpu_encrypt_host then cyaes_gpu_decrypt_host: H2D -> AES -> D2H in %d MiB chunks, "
+                "3 streams" % (chunk >> 20),
+        "encrypt": round(nb / t_e / gib, 2), "decrypt": round(nb / t_d / gib, 2), "enc_plus_dec": round(encdec, 2),
+        "link": link, "frac_of_duplex_link": round(encdec / link["duplex_gibs_per_direction"], 4),
+        "bit_exact": ok,
+    }
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world, err = world_check(args.gpus, os.environ)
+    if err:
+        log("error: " + err)
+        sys.exit(2)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if args.gpus < 1:
+        log("error: --gpus must be >= 1")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # The traffic passes run first, before this process touches the GPU: each
@@ -244,14 +380,17 @@ def main():
     # no process that has initialised the GPU may be the parent of an exec chain.
     live, why = (None, "not requested")
     run_passes, why = traffic_plan(args.traffic, rank, world, args.config, os.environ)
+    if TRAFFIC_ENV in os.environ:  # measured by the launching parent (launch_ranks)
+        handed = json.loads(os.environ[TRAFFIC_ENV])
+        run_passes = False
+        if rank == 0:
+            live, why = handed["traffic"], handed["why"] or "measured by the launching parent"
     if run_passes:
         log("hbm traffic: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (config C) ...")
         live, why = live_traffic()
     import torch
     import torch.distributed as dist
 
-    if world != args.gpus:
-        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     # Rehearsal knobs for a 1-GPU box (never used by the driver): run every rank
     # on device 0 and use gloo instead of RCCL.
     device = 0 if os.environ.get("CYAES_BENCH_SAME_DEVICE") else local
@@ -477,8 +616,9 @@ def main():
             "fill_ms": max_over_ranks(t_fill) / steps * 1e3, "wall_ms": max_over_ranks(t_wall) / steps * 1e3,
             "shards": shards,
         }
-        # leave pass 0's cipher in d_ct for the cpu baseline sample (rank 0 at N=1 walks it)
-        if rank == 0 and world == 1 and mine[0] == 0:
+        # leave pass 0's plaintext and cipher in d_pt / d_ct for the e2e check and the cpu baseline
+        # sample (rank 0 walks pass 0 at every N)
+        if rank == 0 and mine[0] == 0:
             fill(0)
             enc()
         del d_rt
@@ -562,8 +702,18 @@ def main():
         roofline["traffic"] = ftr.get("bytes_per_launch")
         roofline["traffic_note"] = "committed profiles/traffic.json (%s); " % (why,) + str(ftr.get("note"))
 
+    # End to end, PCIe-inclusive (north_star: "the end-to-end rate including
+    # hipMemcpyAsync to and from the device over pinned staging buffers"):
+    # the path starts and ends in host memory (relay_local.cpp:188-217: socket
+    # buffer -> encrypt -> send).  Rank 0 at N = 1, after the timed region.
+    e2e = None
+    if (rank == 0 and world == 1 and args.e2e_gib > 0 and pb == E_PAYLOAD_BYTES and not ppk
+            and main_res.get("d_ct") is not None):
+        log("e2e: host -> device -> host ...")
+        e2e = run_e2e(ctx, torch, main_res["d_pt"], main_res["d_ct"], npay, pb, args.e2e_gib)
+
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         log("cpu baseline ...")
         cpu = cpu_baseline("C (= config E pass 0)" if args.config == "E" else args.config, npay, pb, ppk,
                            main_res["d_ct"], torch, args.cpu_sample)
@@ -688,7 +838,7 @@ def main():
                        "payload_bytes": pb, "parallelism": "payload shards x%d, RCCL key broadcast" % world},
             "hbm_frac_step": round(4.0 * step_bytes / (t / args.steps) / 1e9 / (HBM_PEAK_GBS * world), 4),
             "roofline": roofline, "kernels": kern, "cpu_baseline": cpu, "parity": parity,
-            "packet_configs": packet_configs, "relay_stream": relay,
+            "packet_configs": packet_configs, "relay_stream": relay, "e2e": e2e,
         }
         out["shards"] = main_res["shards"]
         out["dist"] = dict(dist_info, ranks_reporting=len(main_res["shards"]),

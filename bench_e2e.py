@@ -21,6 +21,27 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+def measure(ctx, h_pt, h_ct, h_rt, n, pb, chunk, reps):
+    """Best-of-`reps` seconds of cyaes_gpu_encrypt_host (h_pt -> h_ct) and
+    cyaes_gpu_decrypt_host (h_ct -> h_rt) over n payloads of pb bytes in host
+    memory, after one untimed encrypt that sizes the device slot ring; and
+    whether the round trip restored the plaintext.  Shared with bench.py's `e2e`
+    object."""
+    import torch
+
+    def run(fn, src, dst):
+        t0 = time.perf_counter()
+        fn(src.data_ptr(), dst.data_ptr(), n, pb, chunk_bytes=chunk)
+        return time.perf_counter() - t0
+
+    run(ctx.encrypt_host, h_pt, h_ct)  # first call sizes the device slot ring
+    best_e = best_d = 1e30
+    for _ in range(reps):
+        best_e = min(best_e, run(ctx.encrypt_host, h_pt, h_ct))
+        best_d = min(best_d, run(ctx.decrypt_host, h_ct, h_rt))
+    return best_e, best_d, bool(torch.equal(h_rt, h_pt))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--payloads", type=int, default=131072)
@@ -55,17 +76,7 @@ def main():
     torch.cuda.synchronize()
     del d_tmp
 
-    def run(fn, src, dst):
-        t0 = time.perf_counter()
-        fn(src.data_ptr(), dst.data_ptr(), n, pb, chunk_bytes=chunk)
-        return time.perf_counter() - t0
-
-    run(ctx.encrypt_host, h_pt, h_ct)  # first call sizes the device slot ring
-    best_e = best_d = 1e30
-    for _ in range(args.reps):
-        best_e = min(best_e, run(ctx.encrypt_host, h_pt, h_ct))
-        best_d = min(best_d, run(ctx.decrypt_host, h_ct, h_rt))
-    ok = bool(torch.equal(h_rt, h_pt))
+    best_e, best_d, ok = measure(ctx, h_pt, h_ct, h_rt, n, pb, chunk, args.reps)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     sample = min(n, 64)

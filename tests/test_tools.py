@@ -3,6 +3,7 @@ bench.py's live roofline.traffic and tools/traffic.py share, and the
 corrections MI355X_MICROARCH.md's HBM section prescribes for gfx950
 (counters in kB, FETCH_SIZE counting half the bytes)."""
 import csv
+import json
 import os
 import sys
 
@@ -98,4 +99,67 @@ def test_bench_traffic_plan_and_pass_command(monkeypatch):
     cmd, kw = seen[0]
     assert cmd[0] == sys.executable and cmd[1].endswith("rocprofv3") and cmd[2:4] == ["--pmc", "FETCH_SIZE"]
     assert cmd[cmd.index("--") + 1] == sys.executable
-    assert cmd[-2:] == ["--traffic", "none"] and "RANK" not in kw["env"] and kw["start_new_session"]
+    assert cmd[-2:] == ["--traffic", "none"] and cmd[cmd.index("--e2e-gib") + 1] == "0" and "RANK" not in kw["env"] and kw["start_new_session"]
+
+
+def test_bench_world_size_must_match_gpus():
+    """--gpus N under torchrun must agree with WORLD_SIZE: a
+    mismatch is an error, not a note, so a scaling run cannot silently time a
+    different number of GPUs than it is labelled with."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.world_check(1, {}) == (1, None)
+    assert bench.world_check(8, {}) == (1, None)  # not a rank: bench.py launches the 8 ranks itself
+    assert bench.world_check(4, {"WORLD_SIZE": "4"}) == (4, None)
+    w, err = bench.world_check(8, {"WORLD_SIZE": "1"})
+    assert w == 1 and "--gpus 8 but WORLD_SIZE 1" in err
+
+
+def test_bench_mismatch_exits_nonzero():
+    """The real entry point: WORLD_SIZE=2 with --gpus 1 exits 2 before it
+    imports torch or touches a GPU."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode == 2, p.stderr
+    assert "refusing" in p.stderr and p.stdout == ""
+
+
+def test_bench_launcher_command():
+    """`python bench.py --gpus N` (no torchrun) starts torchrun as a child: N
+    processes on this node, rendezvous on 127.0.0.1, the same arguments."""
+    sys.path.insert(0, ROOT)
+    import bench
+    cmd = bench.launcher_cmd(8, ["--gpus", "8", "--steps", "3"], 29555, python="/py")
+    assert cmd[:3] == ["/py", "-m", "torch.distributed.run"]
+    i = cmd.index("--nproc-per-node")
+    assert cmd[i + 1] == "8" and cmd[cmd.index("--nnodes") + 1] == "1"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and cmd[cmd.index("--master-port") + 1] == "29555"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and cmd[-5].endswith("bench.py")
+
+
+def test_bench_launcher_forwards_rank0_line(monkeypatch, capsys):
+    """launch_ranks: forwards exactly the rank-0 result line (with `launcher`
+    added), sends everything else to stderr, hands the traffic result to the
+    ranks through the environment, and returns the child's exit code."""
+    import argparse
+    sys.path.insert(0, ROOT)
+    import bench
+    script = ("import json, os, sys; print('noise'); print('{not json'); "
+              "t = json.loads(os.environ['%s']); "
+              "print(json.dumps({'metric': %r, 'value': 1.0, 'why': t['why'], 'launched': os.environ['%s']})); "
+              "sys.exit(int(sys.argv[1]))" % (bench.TRAFFIC_ENV, bench.METRIC, bench.LAUNCH_ENV))
+    args = argparse.Namespace(gpus=2, traffic="none", config="E")
+    for rc in (0, 5):
+        monkeypatch.setattr(bench, "launcher_cmd", lambda g, argv, port, _rc=rc: [sys.executable, "-c", script, str(_rc)])
+        assert bench.launch_ranks(args, []) == rc
+        out, err = capsys.readouterr()
+        lines = out.splitlines()
+        assert len(lines) == 1, out
+        d = json.loads(lines[0])
+        assert d["launcher"]["nproc_per_node"] == 2 and d["launched"] == "bench.py" and d["why"] == "not requested"
+        assert "noise" in err and "{not json" in err
+    # ranks that exit 0 without a result line are a failure
+    monkeypatch.setattr(bench, "launcher_cmd", lambda g, argv, port: [sys.executable, "-c", "print('x')"])
+    assert bench.launch_ranks(args, []) == 1

@@ -10,6 +10,8 @@
 #   bench      python bench.py (default: config E headline + packet configs + relay stream)
 #   quickbench bench.py --steps 3 --warmup 1 (no CPU baseline)
 #   profile    rocprofv3 --kernel-trace --stats of a short bench, then FETCH_SIZE / WRITE_SIZE PMC passes
+#   cfgtest    tests/test_config_e.py only (bench.py's own contract and multi-rank runs)
+#   pytest:F   tests/F (a file or file::test), -m gpu
 #   batchertest  tests/test_batcher.py only
 #   batcher    build/bench_batcher SEAL / OPEN loads (host to host), zero-copy and bounce ($BB_ARGS appended)
 #   hostlink   build/hostlink: kernel-driven packet gather/scatter over PCIe vs DMA
@@ -47,12 +49,17 @@ for step in "$@"; do
     quickbench) run quickbench 300 python bench.py --steps 3 --warmup 1 --no-cpu ;;
     profile)
       (cd /tmp && run rocprof_stats 300 rocprofv3 --kernel-trace --stats -d "$O/rocprof" -o run --output-format csv \
-        -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --packet-configs none --relay-stream 0 --traffic none) || exit $?
+        -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --packet-configs none --relay-stream 0 --e2e-gib 0 --traffic none) || exit $?
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && run pmc_$c 300 rocprofv3 --pmc $c -d "$O/pmc_$c" -o run --output-format csv \
           -- python3 "$R/bench.py" --config C --steps 2 --warmup 0 --no-cpu --no-verify --no-clock \
-             --packet-configs none --relay-stream 0 --traffic none) || exit $?
+             --packet-configs none --relay-stream 0 --e2e-gib 0 --traffic none) || exit $?
       done ;;
+    cfgtest) run pytest_config_e 400 python -u -m pytest tests/test_config_e.py -m gpu -x -v --timeout 150 --timeout-method thread ;;
+    pytest:*)  # pytest:FILE[::TEST] -- one test file or test, -m gpu
+      A=${step#pytest:}
+      T=pytest_$(basename "${A%%::*}" .py)
+      run $T 400 python -u -m pytest "tests/$A" -m gpu -x -v --timeout 150 --timeout-method thread ;;
     batchertest) run pytest_batcher 300 python -u -m pytest tests/test_batcher.py -m gpu -x -v --timeout 150 --timeout-method thread ;;
     batcher)  # SEAL / OPEN host to host: zero-copy pools (pointer and offset submits), then the bounce path
       : > "$O/bench_batcher.jsonl"

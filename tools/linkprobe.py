@@ -9,17 +9,13 @@ import argparse
 import json
 import time
 
-import torch
 
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--mib", type=int, default=4096, help="bytes moved per direction")
-    ap.add_argument("--chunk-mib", type=int, default=256)
-    ap.add_argument("--reps", type=int, default=3)
-    a = ap.parse_args()
-    n = a.mib << 20
-    c = a.chunk_mib << 20
+def measure(torch, nbytes, chunk, reps=3):
+    """Pinned host<->device copy ceilings: best-of-`reps` H2D alone, D2H alone
+    and both at once on two streams, `nbytes` per direction in `chunk`-byte
+    copies.  Returns the JSON-able dict (GB/s = 1e9 B/s).  Shared with
+    bench.py's `e2e` object."""
+    n, c = nbytes, chunk
     h_src = torch.empty(n, dtype=torch.uint8, pin_memory=True)
     h_dst = torch.empty(n, dtype=torch.uint8, pin_memory=True)
     h_src.fill_(7)
@@ -39,7 +35,7 @@ def main():
 
     def timed(fns):
         best = 1e30
-        for _ in range(a.reps):
+        for _ in range(reps):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for f in fns:
@@ -51,11 +47,21 @@ def main():
     t_up = timed([h2d])
     t_dn = timed([d2h])
     t_both = timed([h2d, d2h])
-    out = {"bytes_per_direction": n, "chunk_mib": a.chunk_mib,
-           "h2d_gbs": round(n / t_up / 1e9, 2), "d2h_gbs": round(n / t_dn / 1e9, 2),
-           "duplex_gbs_per_direction": round(n / t_both / 1e9, 2),
-           "duplex_gibs_per_direction": round(n / t_both / 2**30, 2)}
-    print(json.dumps(out), flush=True)
+    del h_src, h_dst, d, d2
+    return {"bytes_per_direction": n, "chunk_mib": c >> 20,
+            "h2d_gbs": round(n / t_up / 1e9, 2), "d2h_gbs": round(n / t_dn / 1e9, 2),
+            "duplex_gbs_per_direction": round(n / t_both / 1e9, 2),
+            "duplex_gibs_per_direction": round(n / t_both / 2**30, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mib", type=int, default=4096, help="bytes moved per direction")
+    ap.add_argument("--chunk-mib", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    print(json.dumps(measure(torch, a.mib << 20, a.chunk_mib << 20, a.reps)), flush=True)
 
 
 if __name__ == "__main__":
