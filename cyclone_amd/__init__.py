@@ -77,6 +77,7 @@ _SIGS = {
     "cyaes_gpu_decrypt_ragged": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32,
                                                 _vp, _vp, _vp]),
     "cyaes_gpu_check": (ctypes.c_int, [_vp]),
+    "cyaes_gpu_check_stream": (ctypes.c_int, [_vp, _vp]),
     "cyaes_gpu_encrypt_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                               ctypes.c_uint64]),
     "cyaes_gpu_decrypt_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
@@ -348,10 +349,18 @@ class GpuContext:
                                                 payloads_per_key, chunk_bytes), "decrypt_host")
 
     def check(self):
-        """CYAES_OK, or CYAES_ERANGE if a batch clamped a key index (no raise)."""
+        """CYAES_OK, or CYAES_ERANGE if a batch clamped a key index (no raise).
+        Synchronises the whole device (cyaes_gpu_check)."""
         st = self._lib.cyaes_gpu_check(self._h)
         if st not in (CYAES_OK, CYAES_ERANGE):
             raise CyaesError(st, "check")
+        return st
+
+    def check_stream(self, stream=None):
+        """As check(), waiting for `stream` only (cyaes_gpu_check_stream)."""
+        st = self._lib.cyaes_gpu_check_stream(self._h, _p(stream))
+        if st not in (CYAES_OK, CYAES_ERANGE):
+            raise CyaesError(st, "check_stream")
         return st
 
     def fill_synthetic(self, d_buf, p0, npayloads, payload_bytes, seed, stream=None):

@@ -194,8 +194,15 @@ struct PoolEnt {
     uint8_t* host = nullptr;
     uint64_t dev = 0;
     uint64_t bytes = 0;
-    bool live = false, owned = false;  // owned: registered by us (unregister on removal)
-    uint8_t* pinned = nullptr;         // the page-aligned start we registered
+    bool live = false;
+};
+
+// A page-aligned host range this batcher pinned (hipHostRegister).  Pools
+// whose pages overlap share it: two pools may sit on one page (two buffers of
+// one heap), so a range is unpinned only when no live pool uses it any more.
+struct PinEnt {
+    uintptr_t lo = 0, hi = 0;
+    uint32_t refs = 0;
 };
 
 // Per-thread snapshot of a batcher's session rows and pools, refreshed when
@@ -293,6 +300,8 @@ struct cyaes_batcher {
     // Pools.
     std::mutex pmu;
     std::array<PoolEnt, kMaxPools> pools{};
+    std::array<std::vector<size_t>, kMaxPools> pool_pins;  // pool id -> the PinEnts (indices) it holds
+    std::vector<PinEnt> pins;                                // refs == 0: free entry
     std::atomic<uint64_t> pools_version{1};
 
     const uint64_t id = g_batcher_ids.fetch_add(1);
@@ -313,6 +322,7 @@ struct cyaes_batcher {
     void flush_pending();
     void hand_off(Stage* st);
     int wait_enqueued(const std::array<uint64_t, kShards>& target);
+    void wait_done(const std::array<uint64_t, kShards>& target);
 };
 
 // ---- submission --------------------------------------------------------------
@@ -404,6 +414,9 @@ int cyaes_batcher::make_pooled(const cyaes_pool_req& q, const Snap& ss, Pend* p)
     if (q.pool >= ss.by_id.size() || !ss.by_id[q.pool].live) return CYAES_EINVAL;
     const PoolEnt& e = ss.by_id[q.pool];
     if (q.in_off > e.bytes || (q.op != CYAES_OP_RELAY_OPEN && q.out_off > e.bytes)) return CYAES_EINVAL;
+    // OPEN reads the packet header in make(): the whole packet must lie in the pool first
+    if (q.op == CYAES_OP_RELAY_OPEN && (q.size < CYAES_RELAY_PAYLOAD_OFFSET || q.size > e.bytes - q.in_off))
+        return CYAES_EINVAL;
     cyaes_batch_req r{q.op, q.slot, q.conn_id, e.host + q.in_off,
                       q.op == CYAES_OP_RELAY_OPEN ? e.host + q.in_off : e.host + q.out_off, q.size, q.done, q.user};
     const int st = make(r, ss, p);
@@ -748,8 +761,8 @@ void cyaes_batcher::complete_loop() {
     }
 }
 
-// Waits until every shard has completed `target` requests (flush semantics).
-int cyaes_batcher::wait_enqueued(const std::array<uint64_t, kShards>& target) {
+// Waits until every shard has completed `target` requests; leaves first_error alone.
+void cyaes_batcher::wait_done(const std::array<uint64_t, kShards>& target) {
     std::unique_lock<std::mutex> lk(mu);
     flushers.fetch_add(1);
     cv_submit.notify_all();
@@ -759,6 +772,12 @@ int cyaes_batcher::wait_enqueued(const std::array<uint64_t, kShards>& target) {
         return true;
     });
     flushers.fetch_sub(1);
+}
+
+// Flush semantics: wait, then hand over (and clear) the first error since the previous flush.
+int cyaes_batcher::wait_enqueued(const std::array<uint64_t, kShards>& target) {
+    wait_done(target);
+    std::lock_guard<std::mutex> lk(mu);
     const int err = first_error;
     first_error = CYAES_OK;
     return err;
@@ -890,8 +909,8 @@ void cyaes_batcher_destroy(cyaes_batcher* b) {
     }
     if (b->d_keys) (void)hipFree(b->d_keys);
     if (b->pipe) (void)hipStreamDestroy(b->pipe);
-    for (PoolEnt& p : b->pools)
-        if (p.live && p.owned) (void)hipHostUnregister(p.pinned);
+    for (const PinEnt& p : b->pins)
+        if (p.refs) (void)hipHostUnregister(reinterpret_cast<void*>(p.lo));
     (void)hipSetDevice(dev_prev);
     (void)cyaes_gpu_destroy(b->ctx);
     delete b;
@@ -960,8 +979,88 @@ int cyaes_batcher_session_close(cyaes_batcher* b, uint32_t slot) {
     return CYAES_OK;
 }
 
+// Pins [lo, hi) for a new pool (pmu held, the batcher's device current):
+// pages already pinned by this batcher are shared, the rest are registered
+// here; a range some other owner registered (hipHostMalloc, the caller's own
+// hipHostRegister) is used only if that one registration covers it.  On
+// success `held` lists the PinEnts covering the range, one ref taken on each
+// (unpin() returns them); on failure nothing stays registered.
+static int pin_span(cyaes_batcher* b, uintptr_t lo, uintptr_t hi, std::vector<size_t>* held) {
+    std::vector<std::pair<uintptr_t, uintptr_t>> gaps;  // pages not pinned by this batcher
+    std::vector<size_t> ours;
+    for (size_t i = 0; i < b->pins.size(); i++)
+        if (b->pins[i].refs && b->pins[i].lo < hi && lo < b->pins[i].hi) ours.push_back(i);
+    std::sort(ours.begin(), ours.end(), [&](size_t x, size_t y) { return b->pins[x].lo < b->pins[y].lo; });
+    uintptr_t c = lo;
+    for (size_t i : ours) {
+        if (b->pins[i].lo > c) gaps.push_back({c, b->pins[i].lo});
+        c = std::max(c, b->pins[i].hi);
+    }
+    if (c < hi) gaps.push_back({c, hi});
+    std::vector<PinEnt> added;
+    auto rollback = [&] {
+        for (const PinEnt& p : added) (void)hipHostUnregister(reinterpret_cast<void*>(p.lo));
+        (void)hipGetLastError();
+    };
+    auto registered = [](uintptr_t q, uintptr_t* lo_out, uintptr_t* hi_out) {
+        hipDeviceptr_t rb = nullptr;
+        size_t rs = 0;
+        if (hipMemGetAddressRange(&rb, &rs, reinterpret_cast<hipDeviceptr_t>(q)) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        *lo_out = (uintptr_t)rb;
+        *hi_out = (uintptr_t)rb + rs;
+        return true;
+    };
+    for (const auto& g : gaps) {
+        // Pages someone else registered (hipHostMalloc, the caller's own
+        // hipHostRegister): one such registration must hold the whole gap, and
+        // is then used as it is.  Never register over part of another owner's
+        // registration: HIP then accepts the overlapping range, but unregistering
+        // either one corrupts the other's record (measured: the other owner's
+        // hipHostUnregister fails afterwards).  Checked page by page.
+        uintptr_t rlo = 0, rhi = 0;
+        if (registered(g.first, &rlo, &rhi)) {
+            if (rlo <= g.first && g.second <= rhi) continue;
+            rollback();
+            return CYAES_EINVAL;
+        }
+        for (uintptr_t q = g.first + 4096; q < g.second; q += 4096)
+            if (registered(q, &rlo, &rhi)) {
+                rollback();
+                return CYAES_EINVAL;
+            }
+        void* a = reinterpret_cast<void*>(g.first);
+        const hipError_t e = hipHostRegister(a, g.second - g.first, hipHostRegisterMapped);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            rollback();
+            return map_err(e);
+        }
+        added.push_back(PinEnt{g.first, g.second, 0});
+    }
+    for (size_t i : ours) b->pins[i].refs++;
+    for (const PinEnt& p : added) {
+        size_t i = 0;
+        while (i < b->pins.size() && b->pins[i].refs) i++;
+        if (i == b->pins.size()) b->pins.push_back(p);
+        else b->pins[i] = p;
+        b->pins[i].refs = 1;
+        ours.push_back(i);
+    }
+    *held = ours;
+    return CYAES_OK;
+}
+
+static void unpin(cyaes_batcher* b, const std::vector<size_t>& held) {
+    for (size_t i : held)
+        if (b->pins[i].refs && --b->pins[i].refs == 0) (void)hipHostUnregister(reinterpret_cast<void*>(b->pins[i].lo));
+    (void)hipGetLastError();
+}
+
 int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint32_t* pool) {
-    if (!b || !base || !bytes || !pool) return CYAES_EINVAL;
+    if (!b || !base || !bytes || !pool || (uintptr_t)base + bytes < (uintptr_t)base) return CYAES_EINVAL;
     std::lock_guard<std::mutex> lk(b->pmu);
     int slot = -1;
     for (int i = 0; i < kMaxPools; i++) {
@@ -975,24 +1074,37 @@ int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint
     (void)hipGetDevice(&dev_prev);
     (void)hipSetDevice(b->cfg.device);
     // Pin the whole pages the range covers (the caller's buffer need not be page aligned).
-    uint8_t* lo = reinterpret_cast<uint8_t*>((uintptr_t)base & ~(uintptr_t)4095);
-    const size_t span = (((uintptr_t)base + bytes + 4095) & ~(uintptr_t)4095) - (uintptr_t)lo;
-    bool owned = true;
-    hipError_t e = hipHostRegister(lo, span, hipHostRegisterMapped);
-    if (e == hipErrorHostMemoryAlreadyRegistered) {  // already pinned (hipHostMalloc'd): use it as it is
-        (void)hipGetLastError();
-        owned = false;
-        e = hipSuccess;
-    }
+    const uintptr_t lo = (uintptr_t)base & ~(uintptr_t)4095;
+    const uintptr_t hi = ((uintptr_t)base + bytes + 4095) & ~(uintptr_t)4095;
+    std::vector<size_t> held;
+    int st = pin_span(b, lo, hi, &held);
+    // The device view must be one contiguous range: check it at the end and at
+    // every boundary between the registrations that hold the pool.
     void* dev = nullptr;
-    if (e == hipSuccess) e = hipHostGetDevicePointer(&dev, base, 0);
-    if (e != hipSuccess && owned) (void)hipHostUnregister(lo);
-    (void)hipSetDevice(dev_prev);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        return map_err(e);
+    if (st == CYAES_OK && hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) st = CYAES_EINVAL;
+    if (st == CYAES_OK) {
+        std::vector<uintptr_t> probe{(uintptr_t)base + bytes - 1};
+        for (size_t i : held)
+            for (uintptr_t q : {b->pins[i].lo, b->pins[i].hi - 1, b->pins[i].hi})
+                if (q > (uintptr_t)base && q < (uintptr_t)base + bytes) probe.push_back(q);
+        for (uintptr_t q : probe) {
+            void* dq = nullptr;
+            if (hipHostGetDevicePointer(&dq, reinterpret_cast<void*>(q), 0) != hipSuccess ||
+                (uintptr_t)dq - (uintptr_t)dev != q - (uintptr_t)base) {
+                st = CYAES_EINVAL;
+                break;
+            }
+        }
     }
-    b->pools[slot] = PoolEnt{static_cast<uint8_t*>(base), (uint64_t)(uintptr_t)dev, (uint64_t)bytes, true, owned, lo};
+    if (st != CYAES_OK) {
+        unpin(b, held);
+        (void)hipGetLastError();
+        (void)hipSetDevice(dev_prev);
+        return st;
+    }
+    (void)hipSetDevice(dev_prev);
+    b->pools[slot] = PoolEnt{static_cast<uint8_t*>(base), (uint64_t)(uintptr_t)dev, (uint64_t)bytes, true};
+    b->pool_pins[slot] = std::move(held);
     b->pools_version.fetch_add(1, std::memory_order_release);
     *pool = (uint32_t)slot;
     return CYAES_OK;
@@ -1000,24 +1112,24 @@ int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint
 
 int cyaes_batcher_unregister_pool(cyaes_batcher* b, uint32_t pool) {
     if (!b || pool >= (uint32_t)kMaxPools) return CYAES_EINVAL;
-    PoolEnt ent;
+    std::vector<size_t> held;  // its pins' refs stay taken until the requests below are done
     {
         std::lock_guard<std::mutex> lk(b->pmu);
         if (!b->pools[pool].live) return CYAES_EINVAL;
-        ent = b->pools[pool];
         b->pools[pool].live = false;
+        held = std::move(b->pool_pins[pool]);
+        b->pool_pins[pool].clear();
         b->pools_version.fetch_add(1, std::memory_order_release);
     }
     // Requests enqueued before the removal may still read or write the pool.
-    (void)b->wait_enqueued(enqueue_counts(b));
-    if (ent.owned) {
-        int dev_prev = 0;
-        (void)hipGetDevice(&dev_prev);
-        (void)hipSetDevice(b->cfg.device);
-        const hipError_t e = hipHostUnregister(ent.pinned);
-        (void)hipSetDevice(dev_prev);
-        if (e != hipSuccess) return map_err(e);
-    }
+    // Their errors stay for the next cyaes_batcher_flush (cyaes_batch.h).
+    b->wait_done(enqueue_counts(b));
+    std::lock_guard<std::mutex> lk(b->pmu);
+    int dev_prev = 0;
+    (void)hipGetDevice(&dev_prev);
+    (void)hipSetDevice(b->cfg.device);
+    unpin(b, held);  // pages another live pool still uses stay pinned
+    (void)hipSetDevice(dev_prev);
     return CYAES_OK;
 }
 

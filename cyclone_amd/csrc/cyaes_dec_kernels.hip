@@ -196,9 +196,10 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
 }
 
 // SESS: sessions of payloads_per_key payloads that are whole steps long
-// (a.sess_blocks, a multiple of 64 * R; config D: 256 x 92 blocks): no step
-// straddles two sessions, so the unkeyed step runs under a schedule chosen per
-// step from the scalar block position, and no lane computes a key index.
+// (a.sess_blocks, a multiple of 64 * R; config D: 256 x 92 blocks) and whole
+// ranges long: no range straddles two sessions, so the unkeyed step runs under
+// a schedule chosen per range from the scalar block position, and no lane
+// computes a key index.
 // IV = false: no IV arrays (the relay's calls, cyr_rijndael.cpp:612 with iv =
 // nullptr); the IV code and the payload-index tracking compile out, which
 // keeps the SGPR budget of the round loop (with them, the !BIG SESS kernel
@@ -208,68 +209,66 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     constexpr int R = kDecRows;
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
     fill_dec_image(lds_words, a.tables);
-    unsigned int* leadp = &g_dec_lead[blockIdx.x % kLeadSlots];
+    uint32_t* leadp = dec_lead_word(a.work);
     if (threadIdx.x == 0) *leadp = 0;
     uint32_t prog = 0;
     __syncthreads();
     CLOCK_PROBE(1);
     const uint64_t wave =
         (uint64_t)blockIdx.x * (kDecThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t begin = wave * a.blocks_per_wave;
-    if (begin >= a.nblocks) return;
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lo = dec_lo(threadIdx.x);
-    const uint64_t end = min(begin + a.blocks_per_wave, a.nblocks);
-    FlatPos ps;
-    ps.bp = begin / a.bpp.d;
-    ps.bpos = (uint32_t)(begin - ps.bp * a.bpp.d);
-    uint4 carry = make_uint4(0, 0, 0, 0);  // C[base-1]
-    if (ps.bpos != 0)  // (begin >= 1 here)
-        carry = a.boundary ? LD16(a.boundary + wave, ext(a.boundary, 16ull * gridDim.x * (kDecThreads / 64)))
-                           : LD16(a.in + 16 * (begin - 1), ext(a.in, 16 * a.nblocks));
     uint32_t dk0[44];
     uint32_t dk_id = 0;  // KEYED: session whose schedule dk0 holds (~0u: none yet)
-    uint32_t sess = 0;   // SESS: session of the current step; it ends at block sess_next
-    uint64_t sess_next = 0;
-    if (SESS) {
-        sess = (uint32_t)(begin / a.sess_blocks);
-        sess_next = (uint64_t)(sess + 1) * a.sess_blocks;
-        load_sched(a.keys, sess, 1, dk0);
-    } else if (!KEYED) {
-        load_sched(a.keys, 0, 1, dk0);
-    } else {
-        dk_id = ~0u;
-    }
-    // !BIG: each lane tracks its rows' positions in their payloads, advanced
-    // by step_r per step (one add and a min instead of a division per row;
-    // A/B: config B decrypt ...).
-    uint32_t rk[R];
-    if (!BIG) {
+    if (KEYED) dk_id = ~0u;
+    else if (!SESS) load_sched(a.keys, 0, 1, dk0);
+    // Work ranges [t * range_blocks, +range_blocks): taken from the launch's
+    // ticket counter (dyn), so a wave on a faster CU takes more of them and the
+    // waves finish within about one range of each other; or (static) wave w
+    // takes ranges w, w + nwaves, ...  KEYED (per-lane keys) and IV (IV
+    // arrays): one static range per wave, as the runtime launches them (the
+    // range loop around their larger step bodies cost VGPR spills).
+    const uint32_t nwaves = gridDim.x * (kDecThreads / 64);
+    uint32_t ticket = a.dyn ? next_ticket(a.work) : (uint32_t)wave;
+    while (true) {
+        // The range's parameters are re-read from the kernel arguments here (an
+        // opaque pointer keeps the loads in this block) instead of being held in
+        // SGPRs across the step loop: with them live there the SGPR budget ran
+        // out and the compiler scheduled the steps with 320 s_waitcnt per 640
+        // LDS reads instead of 53.
+        KernArg<DecArgs> ka = (KernArg<DecArgs>)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));
+        if (ticket >= ka->nranges) break;
+        const uint64_t begin = (uint64_t)ticket * ka->range_blocks;
+        const uint64_t end = min(begin + ka->range_blocks, ka->nblocks);
+        FlatPos ps;
+        ps.bp = begin / a.bpp.d;
+        ps.bpos = (uint32_t)(begin - ps.bp * a.bpp.d);
+        uint4 carry = make_uint4(0, 0, 0, 0);  // C[begin-1]
+        if (ps.bpos != 0)  // (begin >= 1 here)
+            carry = ka->boundary ? LD16(ka->boundary + ticket, ext(ka->boundary, 16ull * ka->nranges))
+                                 : LD16(ka->in + 16 * (begin - 1), ext(ka->in, 16 * ka->nblocks));
+        // SESS: a range lies in one session (the runtime makes range_blocks
+        // divide sess_blocks); its schedule is loaded per range (11 loads per
+        // range: tracking the current session kept one more SGPR live and the
+        // compiler spilled VGPRs in the step loop).
+        if (SESS) load_sched(a.keys, (uint32_t)(begin / ka->sess_blocks), 1, dk0);
+        // !BIG: each lane tracks its rows' positions in their payloads, advanced
+        // by step_r per step (one add and a min instead of a division per row).
+        uint32_t rk[R];
+        if (!BIG) {
 #pragma unroll
-        for (int k = 0; k < R; k++) {
-            const uint32_t lpos = ps.bpos + 64 * k + lane;
-            rk[k] = lpos - fastdiv(lpos, a.bpp) * a.bpp.d;
-        }
-    }
-    uint64_t base = begin;
-    uint4 c[R], pv[R];
-    if (base + 64 * R <= end) flat_load<true>(a, lane, base, end, c, pv);
-    // SESS: an outer loop over the wave's sessions, the steps of one session
-    // inside it, so the schedule is invariant in the inner loop.  (Re-loading
-    // it inside the step loop made the compiler schedule the rounds with 321
-    // s_waitcnt per 640 LDS reads against 173.)
-    while (base + 64 * R <= end) {
-        uint64_t stop = end;
-        if (SESS) {
-            if (base >= sess_next) {  // (make_keysel checked every session is in the table)
-                sess++;
-                sess_next += a.sess_blocks;
-                load_sched(a.keys, sess, 1, dk0);
+            for (int k = 0; k < R; k++) {
+                const uint32_t lpos = ps.bpos + 64 * k + lane;
+                const Fastdiv bd = {ka->bpp.M, ka->bpp.d};
+                rk[k] = lpos - fastdiv(lpos, bd) * bd.d;
             }
-            stop = min(end, sess_next);  // sessions are whole steps: base reaches sess_next exactly
         }
-        for (; base + 64 * R <= stop; base += 64 * R) {
+        uint64_t base = begin;
+        uint4 c[R], pv[R];
+        if (base + 64 * R <= end) flat_load<true>(a, lane, base, end, c, pv);
+        for (; base + 64 * R <= end; base += 64 * R) {
             // (Issuing the next step's loads before this step's rounds measured ~1 %
             // slower: the LDS binds, and the other 15 waves hide the loads.)
             carry = flat_step<KEYED, BIG, true, IV>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv, rk);
@@ -286,25 +285,27 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
                 }
             }
         }
-        if (!SESS) break;
-    }
-    if (base < end) {
-        if (SESS && base >= sess_next) load_sched(a.keys, sess + 1, 1, dk0);
-        flat_load<false>(a, lane, base, end, c, pv);
-        flat_step<KEYED, BIG, false, IV>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv, rk);
+        if (base < end) {  // the batch's last, partial step (only the last range has one)
+            flat_load<false>(a, lane, base, end, c, pv);
+            flat_step<KEYED, BIG, false, IV>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv, rk);
+        }
+        if (KEYED || IV) break;
+        ticket = ka->dyn ? next_ticket(ka->work) : ticket + nwaves;
     }
 }
 
-// In-place flat decrypt: snapshot C[begin-1] of every wave range before any
-// wave overwrites it.
-__global__ void k_boundary_snapshot(const uint4* in, uint64_t nblocks, uint64_t bpw, uint64_t nwaves, Fastdiv bpp,
-                                    uint4* boundary) {
-    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= nwaves) return;
-    const uint64_t begin = w * bpw;
+// Before a decrypt (one small launch, stream-ordered): zero the launch's work
+// words, and for an in-place flat decrypt snapshot C[begin-1] of every range
+// before any wave overwrites it.
+__global__ void k_dec_prepass(const uint4* in, uint64_t nblocks, uint64_t range_blocks, uint64_t nranges,
+                              Fastdiv bpp, uint4* boundary, uint32_t* work, uint32_t work_words) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < work_words) work[r] = 0;
+    if (!boundary || r >= nranges) return;
+    const uint64_t begin = r * range_blocks;
     if (begin == 0 || begin >= nblocks) return;
     if (begin % bpp.d != 0)
-        ST16(boundary + w, ext(boundary, 16 * nwaves), LD16(in + (begin - 1), ext(in, 16 * nblocks)));
+        ST16(boundary + r, ext(boundary, 16 * nranges), LD16(in + (begin - 1), ext(in, 16 * nblocks)));
 }
 
 }  // namespace
@@ -326,12 +327,12 @@ hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_boundary_snapshot(const uint8_t* in, uint64_t nblocks, uint64_t blocks_per_wave, uint64_t nwaves,
-                                    Fastdiv bpp, uint4* boundary, hipStream_t stream) {
+hipError_t launch_dec_prepass(const DecArgs& a, uint32_t work_words, hipStream_t stream) {
     const int threads = 256;
-    const int grid = (int)((nwaves + threads - 1) / threads);
-    hipLaunchKernelGGL(k_boundary_snapshot, dim3(grid), dim3(threads), 0, stream,
-                       reinterpret_cast<const uint4*>(in), nblocks, blocks_per_wave, nwaves, bpp, boundary);
+    const uint64_t n = std::max<uint64_t>(work_words, a.boundary ? a.nranges : 0);
+    const int grid = (int)((n + threads - 1) / threads);
+    hipLaunchKernelGGL(k_dec_prepass, dim3(grid), dim3(threads), 0, stream, reinterpret_cast<const uint4*>(a.in),
+                       a.nblocks, a.range_blocks, a.nranges, a.bpp, const_cast<uint4*>(a.boundary), a.work, work_words);
     return hipGetLastError();
 }
 

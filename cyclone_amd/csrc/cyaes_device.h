@@ -238,10 +238,24 @@ __device__ __forceinline__ void fill_dec_image(uint32_t* lds, const uint32_t* __
     }
 }
 // prio_feedback counters of the decrypt workgroups: the 160 KiB image leaves
-// no LDS word free, so they live in global memory (one per workgroup, reset by
-// it at start; a collision between concurrent launches only blurs priorities).
-constexpr uint32_t kLeadSlots = 4096;
-__device__ unsigned int g_dec_lead[kLeadSlots];
+// no LDS word free, so they live in the launch's work words (DecArgs.work,
+// one per workgroup, reset by it at start).
+__device__ __forceinline__ uint32_t* dec_lead_word(uint32_t* work) { return work + kWorkLeadOff + blockIdx.x; }
+
+// A kernel's own arguments in the kernarg segment (constant address space:
+// scalar loads).  Read through an opaque copy of this pointer, a value is
+// loaded where it is used instead of being held in an SGPR across loops.
+template <typename T>
+using KernArg = const __attribute__((address_space(4))) T*;
+
+// The wave's next work ticket (wave-uniform): one atomic on the launch's
+// ticket counter, from the first active lane.
+__device__ __forceinline__ uint32_t next_ticket(uint32_t* ctr) {
+    const uint32_t fl = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
+    uint32_t t = 0;
+    if (__lane_id() == fl) t = atomicAdd(ctr, 1u);
+    return __builtin_amdgcn_readfirstlane(t);
+}
 
 // Decrypts N independent blocks together (N-way ILP per LDS round trip) and
 // returns D(c[n]) ^ prev[n] in prev[n] (CBC, cyr_rijndael.cpp:625-630).

@@ -57,6 +57,10 @@ constexpr uint64_t kQuadRaggedFactor = 1;
 #define CYAES_DEC_ROWS 4
 #endif
 constexpr int kDecRows = CYAES_DEC_ROWS;
+// Dynamic decrypt work (DecArgs.dyn): steps per flat-decrypt range, and the
+// ragged decrypt's payload groups per wave of a full grid.
+constexpr uint32_t kDecRangeSteps = 2;
+constexpr uint32_t kDecGroupsPerWave = 8;
 
 struct Fastdiv {  // Lemire: q = mulhi64(M, n) exact for all 32-bit n, d >= 2
     uint64_t M;
@@ -93,6 +97,13 @@ struct EncArgs {
     uint32_t sess_payloads;  // uniform lane kernel: payloads_per_key when every wave lies in one session (SESS), else 0
 };
 
+// Per-launch decrypt scratch (DecArgs.work): word 0 is the range ticket
+// counter, words kWorkLeadOff + workgroup are the progress-feedback leader
+// words.  Per launch, so concurrent decrypts on different streams never share
+// them.
+constexpr uint32_t kWorkLeadOff = 64;  // its own 256-B line, away from the hot counter
+constexpr uint32_t dec_work_words(uint32_t grid) { return kWorkLeadOff + grid; }
+
 struct DecArgs {
     const uint8_t* in;
     uint8_t* out;
@@ -100,13 +111,16 @@ struct DecArgs {
     const uint32_t* nbytes;
     uint64_t npayloads;
     uint64_t nblocks;         // flat kernel: total blocks = npayloads * bpp
-    uint64_t blocks_per_wave; // flat kernel: contiguous range of one wave
+    uint64_t range_blocks;    // flat kernel: blocks per work range (a multiple of 64*kDecRows)
+    uint64_t nranges;         // flat kernel: ranges; ragged kernel: payload groups
+    uint32_t* work;           // per-launch scratch (dec_work_words, zeroed before the launch): ticket counter, progress words
+    uint32_t dyn;             // 1: waves take ranges / groups from the ticket counter; 0: wave w takes w, w + nwaves, ...
     Fastdiv bpp;              // flat kernel: blocks per payload
     uint32_t step_q, step_r;  // (64*kDecRows) / bpp, % bpp
     KeySel keys;
     const uint8_t* iv_in;
     uint8_t* iv_out;
-    const uint4* boundary;    // flat kernel in-place: C[begin-1] per wave (nullable)
+    const uint4* boundary;    // flat kernel in-place: C[begin-1] per range (nullable)
     uint32_t inplace;         // in == out: drain a step's loads before its stores
     const uint32_t* tables;   // kDecTableWords
     uint32_t* status;
@@ -120,8 +134,9 @@ hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t s
 hipError_t launch_encrypt_quad(const EncArgs& a, int grid, int threads, hipStream_t stream);
 hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, int threads, hipStream_t stream);
-hipError_t launch_boundary_snapshot(const uint8_t* in, uint64_t nblocks, uint64_t blocks_per_wave,
-                                    uint64_t nwaves, Fastdiv bpp, uint4* boundary, hipStream_t stream);
+// Before a decrypt: zeroes its work words and, for an in-place flat decrypt
+// (boundary != NULL), snapshots C[begin-1] of every range that starts inside a payload.
+hipError_t launch_dec_prepass(const DecArgs& a, uint32_t work_words, hipStream_t stream);
 hipError_t launch_key_expand(const uint8_t* d_keys, uint32_t nkeys, const uint8_t* d_sbox,
                              uint32_t* d_sched, hipStream_t stream);
 hipError_t launch_fill_synthetic(uint8_t* buf, uint64_t p0, uint64_t npayloads, uint32_t payload_bytes,

@@ -45,7 +45,7 @@
 //                          k_decrypt_ragged, key expansion, workload utilities,
 //                          the debug readers that sum every TU's records;
 //   cyaes_enc_kernels.hip  (iterative ILP): k_encrypt;
-//   cyaes_dec_kernels.hip  (max ILP): k_decrypt_flat, k_boundary_snapshot.
+//   cyaes_dec_kernels.hip  (max ILP): k_decrypt_flat, k_dec_prepass.
 // Shared device code (access layer, table lookups, rounds, key schedules,
 // priority feedback) is in cyaes_device.h.
 //
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     constexpr int R = kDecRows;
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
     fill_dec_image(lds_words, a.tables);
-    unsigned int* leadp = &g_dec_lead[blockIdx.x % kLeadSlots];
+    uint32_t* leadp = dec_lead_word(a.work);
     if (threadIdx.x == 0) *leadp = 0;
     uint32_t prog = 0;
     __syncthreads();
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     const uint64_t wave0 =
         (uint64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t G = a.group;
-    const uint64_t ngroups = (a.npayloads + G - 1) / G;
+    const uint64_t ngroups = a.nranges;  // (npayloads + G - 1) / G
     const Ext iv_in_e = iv_ext(a.iv_in, a.npayloads), iv_out_e = iv_ext(a.iv_out, a.npayloads);
     uint32_t dk0[44];
     uint32_t dk_id = ~0u;  // session whose schedule dk0 holds
@@ -220,7 +220,10 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         load_sched(a.keys, 0, 1, dk0);
         dk_id = 0;
     }
-    for (uint64_t grp = wave0; grp < ngroups; grp += nwaves) {
+    // Groups from the launch's ticket counter (dyn: a wave on a faster CU takes
+    // more of them), or wave w takes w, w + nwaves, ...
+    for (uint64_t grp = a.dyn ? next_ticket(a.work) : wave0; grp < ngroups;
+         grp = a.dyn ? next_ticket(a.work) : grp + nwaves) {
         const uint64_t p0 = grp * G;
         const uint32_t gn = (uint32_t)min<uint64_t>(G, a.npayloads - p0);
         const bool holder = lane < gn;

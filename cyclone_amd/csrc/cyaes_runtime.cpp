@@ -24,6 +24,10 @@ struct cyaes_gpu {
     uint32_t ragged_group = 0;  // env CYAES_RAGGED_GROUP: payloads per ragged-decrypt wave group (0 = auto; tests, A/B)
     uint32_t enc_run = 0;       // env CYAES_ENC_RUN: payloads per lane run of the uniform encrypt (0 = auto; tests, A/B)
     bool enc_no_sess = false;   // env CYAES_ENC_NO_SESS=1: keyed uniform encrypt always by waterfall (tests, A/B)
+    bool dec_dyn = true;        // env CYAES_DEC_DYN=0: static per-wave decrypt ranges / groups (tests, A/B)
+    uint32_t dec_range_steps = kDecRangeSteps;  // env CYAES_DEC_RANGE_STEPS: steps per dynamic flat-decrypt range
+    uint32_t dec_groups_per_wave = kDecGroupsPerWave;  // env CYAES_DEC_GROUPS_PER_WAVE: ragged groups per wave
+    int dec_grid_max = 0;       // env CYAES_DEC_GRID: cap on decrypt workgroups (tests: many ranges per wave on small batches)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
     uint32_t* d_keys = nullptr;    // nkeys * kSchedWords
     uint32_t nkeys = 0;
@@ -89,7 +93,10 @@ constexpr uint64_t kRunMax = 8;               // payloads per encrypt run
 constexpr uint32_t kRunMaxPayload = 8192;      // runs only for payloads up to 512 blocks
 
 int enc_grid_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kEncWgPerCu); }
-int dec_grid_cap(const cyaes_gpu* ctx) { return std::max(1, ctx->num_cus * kDecWgPerCu); }
+int dec_grid_cap(const cyaes_gpu* ctx) {
+    const int cap = std::max(1, ctx->num_cus * kDecWgPerCu);
+    return ctx->dec_grid_max > 0 ? std::min(cap, ctx->dec_grid_max) : cap;
+}
 
 // Launch shape for `waves` independent wave-sized work items (encrypt: 64
 // chains; ragged decrypt: one payload).  Enough to fill every CU with 16
@@ -227,16 +234,38 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     constexpr int kWaves = kDecThreads / 64;
     const int grid = (int)std::min<uint64_t>((waves_needed + kWaves - 1) / kWaves, (uint64_t)dec_grid_cap(ctx));
     const uint64_t nwaves = (uint64_t)grid * kWaves;
-    uint64_t bpw = (nblocks + nwaves - 1) / nwaves;
+    uint64_t bpw = (nblocks + nwaves - 1) / nwaves;  // the static split: one range per wave
     bpw = (bpw + step - 1) / step * step;
-    StreamScratch iv_copy, boundary;
+    StreamScratch iv_copy, boundary, work;
     st = alias_iv(ctx, iv_copy, &iv_in, iv_out, npayloads, stream);
     if (st) return st;
     a.in = in;
     a.out = out;
     a.npayloads = npayloads;
     a.nblocks = nblocks;
-    a.blocks_per_wave = bpw;
+    // Sessions of payloads_per_key payloads that are whole steps long: every
+    // step lies in one session (the kernel picks its schedule per range).  Only
+    // without IV arrays (the SESS kernels compile the IV code out).
+    const uint64_t sess_blocks = (uint64_t)ppk * bpp;
+    if (!key_idx && ppk && sess_blocks % step == 0 && !iv_in && !iv_out) a.sess_blocks = sess_blocks;
+    // Dynamic ranges of dec_range_steps steps (fewer when the static split is
+    // finer, so a small batch still spreads over every wave), handed out by the
+    // launch's ticket counter: the waves finish within about one range of each
+    // other instead of carrying the spread of CU speeds.
+    // Per-lane keys and IV arrays keep one static range per wave (their kernels
+    // do not loop over ranges).  SESS ranges divide the session.
+    const bool keyed_lane = (key_idx || ppk) && !a.sess_blocks;
+    uint64_t range_steps = bpw / step;
+    a.dyn = ctx->dec_dyn && !keyed_lane && !iv_in && !iv_out && ctx->dec_range_steps > 0 &&
+            ctx->dec_range_steps < range_steps;
+    if (a.dyn) range_steps = ctx->dec_range_steps;
+    if (a.sess_blocks) {
+        const uint64_t sess_steps = a.sess_blocks / step;
+        while (sess_steps % range_steps) range_steps--;
+    }
+    a.range_blocks = range_steps * step;
+    a.nranges = (nblocks + a.range_blocks - 1) / a.range_blocks;
+    if (a.nranges > 0xFFFFFFFFull) return CYAES_EINVAL;  // 32-bit tickets (> 2^40 blocks)
     a.bpp = make_fastdiv(bpp);
     a.step_q = (uint32_t)(step / bpp);
     a.step_r = (uint32_t)(step % bpp);
@@ -245,18 +274,19 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     a.tables = ctx->d_tables + kDecTableOff / 4;
     a.status = ctx->d_status;
     a.inplace = in == out;
-    // Sessions of payloads_per_key payloads that are whole steps long: every
-    // step lies in one session (the kernel picks its schedule per step).  Only
-    // without IV arrays (the SESS kernels compile the IV code out).
-    const uint64_t sess_blocks = (uint64_t)ppk * bpp;
-    if (!key_idx && ppk && sess_blocks % step == 0 && !iv_in && !iv_out) a.sess_blocks = sess_blocks;
-    if (in == out && nwaves > 1) {
-        st = boundary.get(ctx->pool, nwaves * sizeof(uint4), stream);
+    const uint32_t ww = dec_work_words((uint32_t)grid);
+    st = work.get(ctx->pool, 4ull * ww, stream);
+    if (st) return st;
+    a.work = static_cast<uint32_t*>(work.p);
+    if (in == out && a.nranges > 1) {
+        st = boundary.get(ctx->pool, a.nranges * sizeof(uint4), stream);
         if (st) return st;
-        uint4* snap = static_cast<uint4*>(boundary.p);
-        CY_TRY(launch_boundary_snapshot(in, nblocks, bpw, nwaves, a.bpp, snap, stream));
-        a.boundary = snap;
+        a.boundary = static_cast<uint4*>(boundary.p);
     }
+    // The ticket counter (dyn) and the boundary snapshot need the prepass; the
+    // progress words are reset by their workgroups.  A small static batch (the
+    // drop-in's packet) launches the kernel alone, as before.
+    if (a.dyn || a.boundary) CY_TRY(launch_dec_prepass(a, ww, stream));
     return map_err(launch_decrypt_flat(a, grid, stream));
 }
 
@@ -279,15 +309,28 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.tables = ctx->d_tables + kDecTableOff / 4;
     a.status = ctx->d_status;
     a.inplace = in == out;
-    // Payloads per wave group: as many as keep >= 2 groups per wave of a full
-    // grid (balance), up to 64 (one holder lane each); small payloads then
-    // share rows.  Sweep in profiles/r01/ab_ragged_groups.txt.
+    // Payloads per wave group: as many as keep >= dec_groups_per_wave groups per
+    // wave of a full grid (balance: with dynamic groups a wave takes the next
+    // group from the launch's ticket counter, so the finer the groups the closer
+    // the waves finish; static: >= 2), up to 64 (one holder lane each); small
+    // payloads then share rows.  Sweeps in profiles/r01/ab_ragged_groups.txt, r04.
     const uint64_t slots = (uint64_t)std::max(1, ctx->num_cus) * (kDecThreads / 64);
+    const uint64_t per_wave = ctx->dec_dyn ? std::max<uint32_t>(1, ctx->dec_groups_per_wave) : 2;
     const uint64_t G = ctx->ragged_group ? ctx->ragged_group
-                                         : std::min<uint64_t>(64, std::max<uint64_t>(1, npayloads / (2 * slots)));
+                                         : std::min<uint64_t>(64, std::max<uint64_t>(1, npayloads / (per_wave * slots)));
     a.group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, G));
-    const Shape sh = wave_shape(ctx, (npayloads + a.group - 1) / a.group, kDecThreads);
-    return map_err(launch_decrypt_ragged(a, std::min(sh.grid, dec_grid_cap(ctx)), sh.threads, stream));
+    a.nranges = (npayloads + a.group - 1) / a.group;
+    if (a.nranges > 0xFFFFFFFFull) return CYAES_EINVAL;  // 32-bit tickets
+    const Shape sh = wave_shape(ctx, a.nranges, kDecThreads);
+    const int grid = std::min(sh.grid, dec_grid_cap(ctx));
+    a.dyn = ctx->dec_dyn && a.nranges > (uint64_t)grid * (sh.threads / 64);  // more groups than waves
+    StreamScratch work;
+    const uint32_t ww = dec_work_words((uint32_t)grid);
+    st = work.get(ctx->pool, 4ull * ww, stream);
+    if (st) return st;
+    a.work = static_cast<uint32_t*>(work.p);
+    if (a.dyn) CY_TRY(launch_dec_prepass(a, ww, stream));
+    return map_err(launch_decrypt_ragged(a, grid, sh.threads, stream));
 }
 
 bool aligned4(const void* p) { return ((uintptr_t)p & 3u) == 0; }
@@ -364,6 +407,10 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* g = getenv("CYAES_RAGGED_GROUP")) ctx->ragged_group = (uint32_t)strtoul(g, nullptr, 10);
     if (const char* r = getenv("CYAES_ENC_RUN")) ctx->enc_run = (uint32_t)strtoul(r, nullptr, 10);
     if (const char* v = getenv("CYAES_ENC_NO_SESS")) ctx->enc_no_sess = atoi(v) != 0;
+    if (const char* v = getenv("CYAES_DEC_DYN")) ctx->dec_dyn = atoi(v) != 0;
+    if (const char* v = getenv("CYAES_DEC_RANGE_STEPS")) ctx->dec_range_steps = (uint32_t)strtoul(v, nullptr, 10);
+    if (const char* v = getenv("CYAES_DEC_GROUPS_PER_WAVE")) ctx->dec_groups_per_wave = (uint32_t)strtoul(v, nullptr, 10);
+    if (const char* v = getenv("CYAES_DEC_GRID")) ctx->dec_grid_max = atoi(v);
     const HostTables& t = host_tables();
     uint8_t host[kTablesBytes];
     memcpy(host + kEncTableOff, t.enc, sizeof(t.enc));
@@ -584,6 +631,22 @@ int cyaes_gpu_check(cyaes_gpu* ctx) {
     CY_TRY(hipMemcpy(&status, ctx->d_status, 4, hipMemcpyDeviceToHost));
     if (status) {
         CY_TRY(hipMemset(ctx->d_status, 0, 4));
+        return CYAES_ERANGE;
+    }
+    return CYAES_OK;
+}
+
+int cyaes_gpu_check_stream(cyaes_gpu* ctx, void* stream) {
+    if (!ctx) return CYAES_EINVAL;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t status = 0;
+    // All on `stream`: a copy on the null stream would wait for every blocking stream.
+    CY_TRY(hipMemcpyAsync(&status, ctx->d_status, 4, hipMemcpyDeviceToHost, s));
+    CY_TRY(hipStreamSynchronize(s));
+    if (status) {
+        CY_TRY(hipMemsetAsync(ctx->d_status, 0, 4, s));
+        CY_TRY(hipStreamSynchronize(s));
         return CYAES_ERANGE;
     }
     return CYAES_OK;

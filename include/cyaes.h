@@ -154,8 +154,18 @@ int cyaes_gpu_decrypt_host(cyaes_gpu* ctx, const uint8_t* h_in, uint8_t* h_out, 
 /* Synchronises the device (every stream the context's batches ran on) and
  * returns CYAES_EDEVICE on an asynchronous HIP error, CYAES_ERANGE if a batch
  * since the previous check saw an out-of-range key index (the sticky flag is
- * then cleared), else CYAES_OK. */
+ * then cleared), else CYAES_OK.  Cost: hipDeviceSynchronize, so the call
+ * waits for ALL work on the device (other libraries' streams, RCCL, a running
+ * batcher pipeline) and may report a fault another user of the device caused;
+ * that is what charges an asynchronous fault to the check after it.  Hot
+ * paths that check after each batch use cyaes_gpu_check_stream. */
 int cyaes_gpu_check(cyaes_gpu* ctx);
+
+/* The stream-scoped check: waits for `stream` only (NULL: the null stream),
+ * then reads and clears the context's out-of-range flag as cyaes_gpu_check
+ * does.  The flag is per context, so an ERANGE may come from a batch of this
+ * context on another stream that has already finished. */
+int cyaes_gpu_check_stream(cyaes_gpu* ctx, void* stream);
 
 /* ---- Workload utilities (bench / verification; not on the hot path) ----- */
 /* Synthetic plaintext of SURVEY.md §8(d): 64-bit word w of payload p is

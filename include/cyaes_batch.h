@@ -125,12 +125,17 @@ typedef struct cyaes_batch_req {
 } cyaes_batch_req;
 int cyaes_batcher_submit_many(cyaes_batcher* b, const cyaes_batch_req* reqs, uint32_t n, int* status);
 
-/* Packet pools.  register: pins [base, base + bytes) for the device
- * (hipHostRegister, mapped; memory already pinned by hipHostMalloc is used as
- * it is) and returns a pool id; pools may not overlap (CYAES_EINVAL), at most
- * 64 (CYAES_ENOMEM).  unregister: waits until every request submitted before
- * the call has completed, then unpins.  Requests may not use the pool
- * concurrently with its unregister. */
+/* Packet pools.  register: pins the pages of [base, base + bytes) for the
+ * device (hipHostRegister, mapped) and returns a pool id; pools may not
+ * overlap (CYAES_EINVAL), at most 64 (CYAES_ENOMEM).  Pools may share a page
+ * (two buffers of one heap): pages this batcher already pinned are shared and
+ * stay pinned while any live pool uses them.  Memory pinned by someone else
+ * (hipHostMalloc, the caller's hipHostRegister) is used as it is only if one
+ * such registration holds the whole range, else CYAES_EINVAL; the device view
+ * of the pool is checked to be contiguous.  unregister: waits until every
+ * request submitted before the call has completed (their errors are kept for
+ * the next cyaes_batcher_flush), then unpins the pages no other live pool
+ * uses.  Requests may not use the pool concurrently with its unregister. */
 int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint32_t* pool);
 int cyaes_batcher_unregister_pool(cyaes_batcher* b, uint32_t pool);
 

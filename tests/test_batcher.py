@@ -675,14 +675,16 @@ def test_slow_callbacks_keep_order_and_flush_semantics():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("size,recv_copy", [("1472", 1), ("rand:4000", 0), ("rand:65280", 1)])
-def test_relay_loop_both_ends(size, recv_copy):
+@pytest.mark.parametrize("size,recv_copy,depth", [("1472", 1, 2), ("1472", 0, 1), ("rand:4000", 0, 3),
+                                                  ("rand:65280", 1, 2)])
+def test_relay_loop_both_ends(size, recv_copy, depth):
     """tools/relay_loop: the relay's whole data path through the batcher --
     SEAL chunks into per-pipe tunnel streams (packets back to back, as TCP
     carries them; relay_local.cpp:188-217), cut the received stream into
     packets (cye_packet.cpp:166-181), OPEN each in place (relay_server.cpp:329)
     -- and every forwarded payload, RelayForwardMsg field and 0xCE pad byte
-    matches the client's chunk; the wire holds ciphertext."""
+    matches the client's chunk; the wire holds ciphertext.  depth: rounds in
+    flight per looper (1: seal, parse, open in sequence)."""
     import json
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -690,9 +692,118 @@ def test_relay_loop_both_ends(size, recv_copy):
     if not os.path.exists(exe):
         subprocess.run(["make", "-C", root, "-s", "build/relay_loop"], check=True)
     cmd = [exe, "--threads", "3", "--pipes", "4", "--chunks", "8" if size == "rand:65280" else "32",
-           "--size", size, "--recv-copy", str(recv_copy), "--seconds", "0.3"]
+           "--size", size, "--recv-copy", str(recv_copy), "--seconds", "0.3", "--depth", str(depth)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["error"] == 0 and out["mismatches"] == 0
-    assert out["verified"] == out["packets"] > 0 and out["rounds"] > 0
+    assert out["verified"] == out["packets"] > 0 and out["rounds"] > 0 and out["depth"] == depth
+
+
+def test_pools_sharing_a_page(batcher):
+    """Two pools on one page, the second spanning several pages (two buffers of
+    one heap): the shared page stays pinned while either pool
+    lives, so the second pool keeps working after the first is unregistered,
+    on its shared page and on the pages past it."""
+    import numpy as np
+    key = _keys(1, 41)[0]
+    slot = batcher.session_open(key)
+    aes = oracle.Rijndael(key)
+    rng = random.Random(41)
+    buf = np.zeros(8 * 4096, dtype=np.uint8)
+    p0 = (-buf.ctypes.data) % 4096  # first page boundary inside buf
+    a_lo, a_n = p0 + 96, 1024                # pool A: inside page 0
+    b_lo, b_n = p0 + 2048, 3 * 4096 + 512    # pool B: from page 0 into page 3
+    pa = batcher.register_pool(buf[a_lo:a_lo + a_n])
+    pb = batcher.register_pool(buf[b_lo:b_lo + b_n])
+
+    def run(pool, base, spans):
+        want = []
+        reqs = []
+        for off, n in spans:
+            data = bytes(rng.getrandbits(8) for _ in range(n))
+            buf[base + off:base + off + n] = np.frombuffer(data, np.uint8)
+            reqs.append((ca.OP_ENCRYPT, slot, pool, off, off, n, None, 0))
+            want.append((base + off, bytes(aes.encrypt(bytearray(data)))))
+        assert batcher.submit_pooled(reqs) == [0] * len(reqs)
+        assert batcher.flush() == ca.CYAES_OK
+        for o, w in want:
+            assert bytes(buf[o:o + len(w)]) == w
+    run(pa, a_lo, [(0, 512), (512, 512)])
+    run(pb, b_lo, [(0, 1024), (4096, 4096), (b_n - 512, 512)])
+    batcher.unregister_pool(pa)
+    # B's first page is the one A shared; its last bytes are three pages on
+    run(pb, b_lo, [(0, 1008), (b_n - 1024, 1024), (1024, 8192)])
+    # a new pool on the freed part of the shared page shares it again
+    pc = batcher.register_pool(buf[p0:p0 + 2048])
+    run(pc, p0, [(0, 2048)])
+    batcher.unregister_pool(pb)
+    run(pc, p0, [(16, 1024)])
+    batcher.unregister_pool(pc)
+    batcher.session_close(slot)
+
+
+def test_pool_in_foreign_registration(batcher):
+    """Memory someone else pinned is used as it is only when that one
+    registration holds the whole pool: a pool inside it works, one starting in
+    it and reaching past it is refused (CYAES_EINVAL) instead of handing the
+    GPU unmapped pages, and one that starts on unpinned pages and
+    runs into it is refused as well."""
+    import numpy as np
+    import torch
+    cudart = torch.cuda.cudart()
+    if not hasattr(cudart, "cudaHostRegister"):
+        pytest.skip("torch.cuda.cudart() has no cudaHostRegister")
+    key = _keys(1, 43)[0]
+    slot = batcher.session_open(key)
+    buf = np.zeros(8 * 4096, dtype=np.uint8)
+    p0 = (-buf.ctypes.data) % 4096
+    lo = buf.ctypes.data + p0 + 4096  # pages 1..4 of buf's page-aligned part, registered by "someone else"
+    assert int(cudart.cudaHostRegister(lo, 4 * 4096, 0)) == 0
+    key_aes = oracle.Rijndael(key)
+
+    def encrypt_in(pid, base, n, seed):
+        data = bytes(random.Random(seed).getrandbits(8) for _ in range(n))
+        buf[base:base + n] = np.frombuffer(data, np.uint8)
+        assert batcher.submit_pooled([(ca.OP_ENCRYPT, slot, pid, 0, 0, n, None, 0)]) == [0]
+        assert batcher.flush() == ca.CYAES_OK
+        assert bytes(buf[base:base + n]) == bytes(key_aes.encrypt(bytearray(data)))
+    try:
+        # starts inside the foreign registration and runs past it: refused
+        with pytest.raises(ca.CyaesError):
+            batcher.register_pool(buf[p0 + 4096:p0 + 6 * 4096])
+        # starts on a page nobody pinned and runs into the registration: refused too
+        # (registering over part of another owner's registration corrupts its record)
+        with pytest.raises(ca.CyaesError):
+            batcher.register_pool(buf[p0 + 100:p0 + 3 * 4096])
+        # pages nobody pinned, next to the registration: the batcher pins them itself
+        pid = batcher.register_pool(buf[p0 + 5 * 4096 + 16:p0 + 7 * 4096])
+        encrypt_in(pid, p0 + 5 * 4096 + 16, 4096, 42)
+        batcher.unregister_pool(pid)
+        # inside the foreign registration: used as it is
+        pid = batcher.register_pool(buf[p0 + 4096 + 64:p0 + 5 * 4096 - 64])
+        encrypt_in(pid, p0 + 4096 + 64, 4096, 43)
+        batcher.unregister_pool(pid)  # leaves the foreign registration alone
+    finally:
+        assert int(cudart.cudaHostUnregister(lo)) == 0
+    batcher.session_close(slot)
+
+
+def test_pooled_open_range_and_unregister_flush(batcher):
+    """A pooled OPEN whose packet would run past its pool is refused before
+    its header is read, and unregister_pool, which drains the
+    requests before it, leaves flush's error hand-off to flush."""
+    import numpy as np
+    assert batcher.flush() == ca.CYAES_OK
+    key = _keys(1, 45)[0]
+    slot = batcher.session_open(key)
+    pool = np.zeros(1 << 16, dtype=np.uint8)
+    pid = batcher.register_pool(pool)
+    # an OPEN whose packet is not a RELAY_FORWARD packet is refused at submit (no batch error) ...
+    assert batcher.submit_pooled([(ca.OP_RELAY_OPEN, slot, pid, 0, 0, 64, None, 0)]) == [ca.CYAES_EINVAL]
+    # ... and one that would read its header past the pool's end is refused before it reads
+    assert batcher.submit_pooled([(ca.OP_RELAY_OPEN, slot, pid, pool.size - 2, 0, 64, None, 0)]) == \
+        [ca.CYAES_EINVAL]
+    batcher.unregister_pool(pid)
+    assert batcher.flush() == ca.CYAES_OK
+    batcher.session_close(slot)

@@ -33,9 +33,17 @@ def torch():
 # single payloads where runs do not apply: IV arrays, key index arrays,
 # sessions that are not whole runs).  The full-size configs below use the
 # runtime's own choice.
+# Decrypt: waves take work ranges (flat kernel) and payload
+# groups (ragged kernel) from a per-launch ticket counter once a wave has more
+# than one; "dyn1" caps the decrypt grid at 3 workgroups with 1-step ranges,
+# so even the small test batches hand out many ranges per wave, and "static1"
+# runs the static per-wave split on a 2-workgroup grid.
 KERNEL_MODES = {"auto": {}, "lane": {"CYAES_QUAD_MAX_CHAINS": "0"},
-                "run3": {"CYAES_QUAD_MAX_CHAINS": "0", "CYAES_ENC_RUN": "3"}}
-_MODE_VARS = ("CYAES_QUAD_MAX_CHAINS", "CYAES_ENC_RUN")
+                "run3": {"CYAES_QUAD_MAX_CHAINS": "0", "CYAES_ENC_RUN": "3"},
+                "dyn1": {"CYAES_DEC_GRID": "3", "CYAES_DEC_RANGE_STEPS": "1", "CYAES_DEC_GROUPS_PER_WAVE": "64"},
+                "static1": {"CYAES_QUAD_MAX_CHAINS": "0", "CYAES_DEC_GRID": "2", "CYAES_DEC_DYN": "0"}}
+_MODE_VARS = ("CYAES_QUAD_MAX_CHAINS", "CYAES_ENC_RUN", "CYAES_DEC_GRID", "CYAES_DEC_RANGE_STEPS",
+              "CYAES_DEC_GROUPS_PER_WAVE", "CYAES_DEC_DYN")
 
 
 def _set_mode(mode):
@@ -242,6 +250,75 @@ def test_in_place_decrypts_on_two_streams(torch, ctx):
     assert ctx.check() == ca.CYAES_OK
 
 
+@pytest.mark.parametrize("pb,n", [(1472, 65536), (65536, 2048), (1488, 40000)])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_dynamic_ranges_full_grid(torch, pb, n, inplace):
+    """Flat decrypt with the default grid on batches big enough that each wave
+    takes several work ranges from the launch's ticket counter (DESIGN.md §3.3,
+    VERDICT r03 next 2): MTU payloads (!BIG rows), 64 KiB payloads (one payload
+    start per step at most), and a payload size that does not divide a step.
+    In place, every range's C[begin-1] comes from the prepass snapshot.  The
+    same batch under the static per-wave split gives the same bytes."""
+    pt = oracle.synthetic(11, n, pb)
+    ct = oracle.batch(False, [K0], 0, pt, pb, nthreads=16)
+    outs = []
+    for env in ({}, {"CYAES_DEC_DYN": "0"}, {"CYAES_DEC_RANGE_STEPS": "1"}, {"CYAES_DEC_RANGE_STEPS": "5"}):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        c = ca.GpuContext(0)
+        _restore(old)
+        c.set_keys(K0)
+        d = dev(torch, ct)
+        out = d if inplace else empty(torch, ct.size)
+        c.decrypt_uniform(d, out, n, pb)
+        outs.append(host(out))
+        assert c.check() == ca.CYAES_OK
+        c.close()
+    for o in outs:
+        assert np.array_equal(o, pt)
+
+
+def test_concurrent_flat_and_ragged_decrypts(torch):
+    """A flat and a ragged decrypt (and two flat ones) on two streams at once,
+    repeatedly: each launch has its own ticket counter and progress words
+    (DecArgs.work), so neither disturbs the other (VERDICT r03 weak 7 / next 6;
+    the relay decrypts on its loopers, relay_server.cpp:329, while a drop-in
+    caller decrypts, cyr_rijndael.cpp:612-635)."""
+    pb, n = 1472, 65536
+    hdr, stride = 12, pb + 12
+    c = ca.GpuContext(0)
+    c.set_keys(K0)
+    pt = oracle.synthetic(21, n, pb)
+    ct = oracle.batch(False, [K0], 0, pt, pb, nthreads=16)
+    flat = dev(torch, ct)
+    flat2 = dev(torch, ct)
+    stream_buf = np.full(n * stride + 16, 0xA5, np.uint8)
+    stream_buf[:n * stride].reshape(n, stride)[:, hdr:hdr + pb] = ct.reshape(n, pb)
+    rbuf = dev(torch, stream_buf)
+    off = dev(torch, np.arange(n, dtype=np.uint64) * stride + hdr)
+    nb = dev(torch, np.full(n, pb, np.uint32))
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for rep in range(4):  # decrypt, then encrypt back, on both streams, both orders
+        a, b = (s1, s2) if rep % 2 == 0 else (s2, s1)
+        c.decrypt_uniform(flat, flat, n, pb, stream=a.cuda_stream)
+        c.decrypt_ragged(rbuf, rbuf, off, nb, n, stream=b.cuda_stream)
+        c.decrypt_uniform(flat2, flat2, n, pb, stream=b.cuda_stream)
+        c.encrypt_uniform(flat, flat, n, pb, stream=a.cuda_stream)
+        c.encrypt_ragged(rbuf, rbuf, off, nb, n, stream=b.cuda_stream)
+        c.encrypt_uniform(flat2, flat2, n, pb, stream=b.cuda_stream)
+    c.decrypt_uniform(flat, flat, n, pb, stream=s1.cuda_stream)
+    c.decrypt_ragged(rbuf, rbuf, off, nb, n, stream=s2.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(flat), pt)
+    assert np.array_equal(host(flat2), ct)
+    got = host(rbuf)
+    assert np.array_equal(got[:n * stride].reshape(n, stride)[:, hdr:hdr + pb].reshape(-1), pt)
+    assert (got[:n * stride].reshape(n, stride)[:, :hdr] == 0xA5).all()
+    assert c.check() == ca.CYAES_OK
+    c.close()
+
+
 def test_session_keys_payloads_per_key(torch, ctx):
     """Config D shape, scaled: keys grouped by payload (payload p uses key p / ppk)."""
     nk, ppk, pb = 24, 7, 1472
@@ -354,6 +431,16 @@ def test_key_index_array_divergent_waves(torch, encrypt_kernel):
     c.encrypt_uniform(d_pt, d_ct, n, pb, key_idx=dev(torch, bad))
     assert c.check() == ca.CYAES_ERANGE  # reported, then cleared
     assert c.check() == ca.CYAES_OK
+    # the stream-scoped check (waits for that stream only) reports and clears the same flag
+    s = torch.cuda.Stream()
+    d_bad = dev(torch, bad)
+    s.wait_stream(torch.cuda.current_stream())
+    c.encrypt_uniform(d_pt, d_ct, n, pb, key_idx=d_bad, stream=s.cuda_stream)
+    assert c.check_stream(s.cuda_stream) == ca.CYAES_ERANGE
+    assert c.check_stream(s.cuda_stream) == ca.CYAES_OK and c.check() == ca.CYAES_OK
+    c.encrypt_uniform(d_pt, d_ct, n, pb, key_idx=d_k, stream=s.cuda_stream)
+    assert c.check_stream(s.cuda_stream) == ca.CYAES_OK
+    assert np.array_equal(host(d_ct), want)
     c.close()
 
 

@@ -5,6 +5,8 @@ Each case draws a batch shape, key mode, IV mode and layout from a seeded
 generator and forces the kernel choice through the runtime's A/B knobs:
   encrypt  CYAES_QUAD_MAX_CHAINS   lane per chain / four lanes per chain
   decrypt  CYAES_RAGGED_GROUP      payloads per wave group of the ragged kernel
+           CYAES_DEC_GRID / CYAES_DEC_RANGE_STEPS / CYAES_DEC_DYN   work ranges from the
+           ticket counter on a small grid, or the static per-wave split
 Layouts: uniform (flat decrypt, incl. the session-aligned keyed path) and
 ragged relay-packet streams (payload at packet offset 12, gaps, empties).
 Semantics: Rijndael::encrypt/decrypt per payload (cyr_rijndael.cpp:588-635),
@@ -71,7 +73,11 @@ def draw_case(seed):
         rng=rng, layout=layout, n=n, blocks=blocks, keying=keying, ppk=ppk,
         iv_in=bool(rng.integers(0, 2)), iv_out=bool(rng.integers(0, 2)), inplace=bool(rng.integers(0, 2)),
         env={"CYAES_QUAD_MAX_CHAINS": str(rng.choice(["0", str(1 << 40)])) if rng.integers(0, 3) else None,
-             "CYAES_RAGGED_GROUP": str(rng.choice([1, 2, 5, 64])) if rng.integers(0, 3) else None})
+             "CYAES_RAGGED_GROUP": str(rng.choice([1, 2, 5, 64])) if rng.integers(0, 3) else None,
+             # decrypt work distribution: a small grid with 1- or 3-step ticket ranges, or the static split
+             "CYAES_DEC_GRID": str(rng.choice([1, 2, 5])) if rng.integers(0, 2) else None,
+             "CYAES_DEC_RANGE_STEPS": str(rng.choice([1, 3])) if rng.integers(0, 2) else None,
+             "CYAES_DEC_DYN": "0" if rng.integers(0, 4) == 0 else None})
 
 
 @pytest.mark.parametrize("seed", range(NCASES))

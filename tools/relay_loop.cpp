@@ -26,6 +26,7 @@
 //
 // usage: relay_loop [--threads T] [--pipes P] [--chunks K] [--size B | --size rand:MAX]
 //                   [--seconds S] [--recv-copy 0|1] [--verify 0|1] [--batch-mb M] [--delay-us D]
+//                   [--depth R]  (rounds in flight per looper; 1 = seal, parse, open in sequence)
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -52,13 +53,21 @@ uint64_t splitmix(uint64_t& x) {
     return z ^ (z >> 31);
 }
 
+struct Slot {  // one round in flight: its tunnel streams and chunk sizes
+    uint64_t tx_off = 0, rx_off = 0;
+    std::vector<uint32_t> size;  // per (pipe, chunk)
+    std::vector<uint64_t> len;   // per pipe: stream bytes
+    uint64_t round = 0;
+};
+
 struct Looper {
     int id = 0;
     cyaes_batcher* b = nullptr;
-    uint32_t pipes = 0, chunks = 0, max_chunk = 0, rand_size = 0, fixed_size = 0;
+    uint32_t pipes = 0, chunks = 0, max_chunk = 0, rand_size = 0, fixed_size = 0, depth = 2;
     bool recv_copy = true, verify = true;
     uint8_t* mem = nullptr;
-    uint64_t src_off = 0, tx_off = 0, rx_off = 0, pipe_stream = 0;
+    uint64_t src_off = 0, pipe_stream = 0;
+    std::vector<Slot> slots;
     uint32_t pool = 0;
     std::vector<uint32_t> slot;  // per pipe: session slot (one secret, both ends)
     uint64_t packets = 0, payload = 0, rounds = 0, verified = 0, mismatches = 0;
@@ -66,13 +75,14 @@ struct Looper {
     uint64_t rng = 0;
 };
 
-// Waits for n completions of this thread's requests (poll mode).
+// Waits for n completions of this thread's requests (poll mode).  A thread's
+// requests complete in submission order, so the n are the oldest n.
 int drain(cyaes_batcher* b, uint64_t n) {
     void* users[256];
     int status[256];
     int err = CYAES_OK;
     while (n) {
-        const uint32_t got = cyaes_batcher_poll(b, users, status, 256);
+        const uint32_t got = cyaes_batcher_poll(b, users, status, (uint32_t)std::min<uint64_t>(n, 256));
         for (uint32_t i = 0; i < got; i++)
             if (status[i] && err == CYAES_OK) err = status[i];
         n -= got;
@@ -81,99 +91,135 @@ int drain(cyaes_batcher* b, uint64_t n) {
     return err;
 }
 
-// Rounds until `until` (at least min_rounds).
-void run(Looper* L, Clock::time_point until, uint64_t min_rounds) {
+int submit(Looper* L, std::vector<cyaes_pool_req>& reqs) {
+    std::vector<int> status(reqs.size(), 0);
+    if (cyaes_batcher_submit_pooled(L->b, reqs.data(), (uint32_t)reqs.size(), status.data()) != CYAES_OK)
+        return *std::find_if(status.begin(), status.end(), [](int s) { return s != 0; });
+    return CYAES_OK;
+}
+
+// local end: SEAL chunk k of pipe p (source bytes at a fixed spot) into the pipe's tunnel stream
+int seal(Looper* L, Slot& S) {
     const uint32_t P = L->pipes, K = L->chunks;
-    std::vector<uint32_t> size(P * K);
-    std::vector<uint64_t> len(P);
     std::vector<cyaes_pool_req> reqs;
-    std::vector<int> status;
+    reqs.reserve(P * K);
+    std::fill(S.len.begin(), S.len.end(), 0);
+    for (uint32_t k = 0; k < K; k++)
+        for (uint32_t p = 0; p < P; p++) {
+            const uint32_t n = L->rand_size ? 1 + (uint32_t)(splitmix(L->rng) % L->rand_size) : L->fixed_size;
+            S.size[p * K + k] = n;
+            const uint64_t src = L->src_off + (uint64_t)(p * K + k) * L->max_chunk;
+            const uint64_t dst = S.tx_off + p * L->pipe_stream + S.len[p];
+            reqs.push_back({CYAES_OP_RELAY_SEAL, L->slot[p], (int32_t)(1000 * L->id + p), L->pool, src, dst, n,
+                            nullptr, nullptr});
+            S.len[p] += cyaes_relay_packet_bytes(n);
+        }
+    return submit(L, reqs);
+}
+
+// the tunnel: the server end receives the stream (a socket copy), cuts it into packets, OPENs them
+int open_round(Looper* L, Slot& S) {
+    const uint32_t P = L->pipes, K = L->chunks;
+    if (L->verify)  // on the wire: ciphertext, not the chunk (each pipe's first packet)
+        for (uint32_t p = 0; p < P; p++) {
+            const uint32_t n = S.size[p * K];
+            const uint8_t* pkt = L->mem + S.tx_off + p * L->pipe_stream;
+            const uint8_t* chunk = L->mem + L->src_off + (uint64_t)(p * K) * L->max_chunk;
+            L->mismatches += n >= 16 && memcmp(pkt + CYAES_RELAY_PAYLOAD_OFFSET, chunk, 16) == 0;
+        }
+    std::vector<cyaes_pool_req> reqs;
+    reqs.reserve(P * K);
     std::vector<uint64_t> offs(K + 1);
     std::vector<uint32_t> psz(K + 1);
     std::vector<uint16_t> pid(K + 1);
-    reqs.reserve(P * K);
-    for (uint64_t r = 0; (r < min_rounds || Clock::now() < until) && L->err == CYAES_OK; r++) {
-        // local end: SEAL chunk k of pipe p (source bytes at a fixed spot) into the pipe's tunnel stream
-        reqs.clear();
-        std::fill(len.begin(), len.end(), 0);
+    for (uint32_t p = 0; p < P; p++) {
+        uint8_t* tx = L->mem + S.tx_off + p * L->pipe_stream;
+        const uint64_t rbase = (L->recv_copy ? S.rx_off : S.tx_off) + p * L->pipe_stream;
+        if (L->recv_copy) memcpy(L->mem + rbase, tx, S.len[p]);
+        size_t used = 0;
+        const uint32_t np = cyaes_relay_parse(L->mem + rbase, S.len[p], offs.data(), psz.data(), pid.data(), K + 1, &used);
+        if (np != K || used != S.len[p]) {
+            fprintf(stderr, "looper %d pipe %u: parsed %u packets over %zu of %llu bytes\n", L->id, p, np, used,
+                    (unsigned long long)S.len[p]);
+            return CYAES_EINVAL;
+        }
         for (uint32_t k = 0; k < K; k++)
-            for (uint32_t p = 0; p < P; p++) {
-                const uint32_t n = L->rand_size ? 1 + (uint32_t)(splitmix(L->rng) % L->rand_size) : L->fixed_size;
-                size[p * K + k] = n;
-                const uint64_t src = L->src_off + (uint64_t)(p * K + k) * L->max_chunk;
-                const uint64_t dst = L->tx_off + p * L->pipe_stream + len[p];
-                reqs.push_back({CYAES_OP_RELAY_SEAL, L->slot[p], (int32_t)(1000 * L->id + p), L->pool, src, dst, n,
-                                nullptr, nullptr});
-                len[p] += cyaes_relay_packet_bytes(n);
+            reqs.push_back({CYAES_OP_RELAY_OPEN, L->slot[p], 0, L->pool, rbase + offs[k], 0,
+                            CYAES_RELAY_HEADSIZE + psz[k], nullptr, nullptr});
+    }
+    return submit(L, reqs);
+}
+
+// the target: what relay_server forwards must be the client's chunk
+void check_round(Looper* L, const Slot& S) {
+    const uint32_t P = L->pipes, K = L->chunks;
+    for (uint32_t p = 0; p < P; p++) {
+        const uint64_t rbase = (L->recv_copy ? S.rx_off : S.tx_off) + p * L->pipe_stream;
+        uint64_t o = 0;
+        for (uint32_t k = 0; k < K; k++) {
+            const uint32_t n = S.size[p * K + k];
+            if (L->verify) {
+                const uint8_t* pkt = L->mem + rbase + o;
+                const uint8_t* chunk = L->mem + L->src_off + (uint64_t)(p * K + k) * L->max_chunk;
+                bool ok = cyaes_relay_forward_id(pkt) == (int32_t)(1000 * L->id + p) &&
+                          cyaes_relay_forward_size(pkt) == (int32_t)n &&
+                          memcmp(pkt + CYAES_RELAY_PAYLOAD_OFFSET, chunk, n) == 0;
+                for (uint32_t i = n; i < cyaes_relay_round16(n); i++)  // the 0xCE padding decrypts back too
+                    ok = ok && pkt[CYAES_RELAY_PAYLOAD_OFFSET + i] == CYAES_RELAY_PAD;
+                L->mismatches += !ok;
+                L->verified++;
             }
-        status.assign(reqs.size(), 0);
-        if (cyaes_batcher_submit_pooled(L->b, reqs.data(), (uint32_t)reqs.size(), status.data()) != CYAES_OK) {
-            L->err = *std::find_if(status.begin(), status.end(), [](int s) { return s != 0; });
-            return;
+            o += cyaes_relay_packet_bytes(n);
+            L->payload += n;
         }
-        if ((L->err = drain(L->b, reqs.size())) != CYAES_OK) return;
-        if (L->verify)  // on the wire: ciphertext, not the chunk (each pipe's first packet)
-            for (uint32_t p = 0; p < P; p++) {
-                const uint32_t n = size[p * K];
-                const uint8_t* pkt = L->mem + L->tx_off + p * L->pipe_stream;
-                const uint8_t* chunk = L->mem + L->src_off + (uint64_t)(p * K) * L->max_chunk;
-                L->mismatches += n >= 16 && memcmp(pkt + CYAES_RELAY_PAYLOAD_OFFSET, chunk, 16) == 0;
-            }
-        // the tunnel: the server end receives the stream (a socket copy) and cuts it into packets
-        reqs.clear();
-        for (uint32_t p = 0; p < P; p++) {
-            uint8_t* tx = L->mem + L->tx_off + p * L->pipe_stream;
-            const uint64_t rbase = (L->recv_copy ? L->rx_off : L->tx_off) + p * L->pipe_stream;
-            if (L->recv_copy) memcpy(L->mem + rbase, tx, len[p]);
-            size_t used = 0;
-            const uint32_t np =
-                cyaes_relay_parse(L->mem + rbase, len[p], offs.data(), psz.data(), pid.data(), K + 1, &used);
-            if (np != K || used != len[p]) {
-                fprintf(stderr, "looper %d pipe %u: parsed %u packets over %zu of %llu bytes\n", L->id, p, np, used,
-                        (unsigned long long)len[p]);
-                L->err = CYAES_EINVAL;
-                return;
-            }
-            for (uint32_t k = 0; k < K; k++)
-                reqs.push_back({CYAES_OP_RELAY_OPEN, L->slot[p], 0, L->pool, rbase + offs[k], 0,
-                                CYAES_RELAY_HEADSIZE + psz[k], nullptr, nullptr});
-        }
-        status.assign(reqs.size(), 0);
-        if (cyaes_batcher_submit_pooled(L->b, reqs.data(), (uint32_t)reqs.size(), status.data()) != CYAES_OK) {
-            L->err = *std::find_if(status.begin(), status.end(), [](int s) { return s != 0; });
-            return;
-        }
-        if ((L->err = drain(L->b, reqs.size())) != CYAES_OK) return;
-        // the target: what relay_server forwards must be the client's chunk
-        for (uint32_t p = 0; p < P; p++) {
-            const uint64_t rbase = (L->recv_copy ? L->rx_off : L->tx_off) + p * L->pipe_stream;
-            uint64_t o = 0;
-            for (uint32_t k = 0; k < K; k++) {
-                const uint32_t n = size[p * K + k];
-                if (L->verify) {
-                    const uint8_t* pkt = L->mem + rbase + o;
-                    const uint8_t* chunk = L->mem + L->src_off + (uint64_t)(p * K + k) * L->max_chunk;
-                    bool ok = cyaes_relay_forward_id(pkt) == (int32_t)(1000 * L->id + p) &&
-                              cyaes_relay_forward_size(pkt) == (int32_t)n &&
-                              memcmp(pkt + CYAES_RELAY_PAYLOAD_OFFSET, chunk, n) == 0;
-                    for (uint32_t i = n; i < cyaes_relay_round16(n); i++)  // the 0xCE padding decrypts back too
-                        ok = ok && pkt[CYAES_RELAY_PAYLOAD_OFFSET + i] == CYAES_RELAY_PAD;
-                    L->mismatches += !ok;
-                    L->verified++;
-                }
-                o += cyaes_relay_packet_bytes(n);
-                L->payload += n;
+    }
+    L->packets += (uint64_t)P * K;
+    L->rounds++;
+}
+
+// Rounds until `until` (at least min_rounds), `depth` rounds in flight: each
+// looper keeps `depth` slots, and while the GPU seals or opens one slot's
+// packets the looper parses, submits or checks another's.  A looper's requests
+// complete in submission order, so it drains them group by group: a sealed
+// round is parsed and opened, an opened round is checked and its slot sealed
+// again with the next round (depth 1: the sequential seal -> parse -> open).
+void run(Looper* L, Clock::time_point until, uint64_t min_rounds) {
+    struct Group {
+        bool open;
+        uint32_t slot;
+    };
+    std::vector<Group> fifo;  // groups in flight, oldest first
+    size_t head = 0;
+    const uint64_t n = (uint64_t)L->pipes * L->chunks;
+    uint64_t next_round = 0;
+    auto more = [&] { return next_round < min_rounds || Clock::now() < until; };
+    for (uint32_t s = 0; s < L->depth && more(); s++) {
+        L->slots[s].round = next_round++;
+        if ((L->err = seal(L, L->slots[s])) != CYAES_OK) return;
+        fifo.push_back({false, s});
+    }
+    while (head < fifo.size()) {
+        const Group g = fifo[head++];
+        if ((L->err = drain(L->b, n)) != CYAES_OK) return;
+        Slot& S = L->slots[g.slot];
+        if (!g.open) {
+            if ((L->err = open_round(L, S)) != CYAES_OK) return;
+            fifo.push_back({true, g.slot});
+        } else {
+            check_round(L, S);
+            if (more()) {
+                S.round = next_round++;
+                if ((L->err = seal(L, S)) != CYAES_OK) return;
+                fifo.push_back({false, g.slot});
             }
         }
-        L->packets += (uint64_t)P * K;
-        L->rounds++;
     }
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
-    uint32_t threads = 8, pipes = 16, chunks = 256, batch_mb = 32, delay_us = 100, recv_copy = 1, verify = 1;
+    uint32_t threads = 8, pipes = 16, chunks = 256, batch_mb = 32, delay_us = 100, recv_copy = 1, verify = 1, depth = 2;
     std::string size_arg = "1472";
     double seconds = 4;
     for (int i = 1; i + 1 < argc; i += 2) {
@@ -187,11 +233,12 @@ int main(int argc, char** argv) {
         else if (a == "--verify") verify = atoi(argv[i + 1]);
         else if (a == "--batch-mb") batch_mb = atoi(argv[i + 1]);
         else if (a == "--delay-us") delay_us = atoi(argv[i + 1]);
+        else if (a == "--depth") depth = atoi(argv[i + 1]);
     }
     uint32_t rand_size = 0, fixed_size = 0;
     if (size_arg.rfind("rand:", 0) == 0) rand_size = std::min<uint32_t>(atoi(size_arg.c_str() + 5), CYAES_RELAY_MAX_CHUNK);
     else fixed_size = std::min<uint32_t>(atoi(size_arg.c_str()), CYAES_RELAY_MAX_CHUNK);
-    if (!threads || threads > 16 || !pipes || !chunks || (!rand_size && !fixed_size)) {  // 16 shards: one queue each
+    if (!threads || threads > 16 || !pipes || !chunks || (!rand_size && !fixed_size) || !depth || depth > 8) {  // 16 shards: one queue each
         fprintf(stderr, "bad arguments\n");
         return 1;
     }
@@ -216,19 +263,28 @@ int main(int argc, char** argv) {
         l.recv_copy = recv_copy != 0;
         l.verify = verify != 0;
         l.rng = 0x5EEDC1C1ull + t;
+        l.depth = depth;
         l.pipe_stream = ((uint64_t)chunks * cyaes_relay_packet_bytes(max_chunk) + 4095) & ~4095ull;
         const uint64_t src = (uint64_t)pipes * chunks * max_chunk;
         l.src_off = 0;
-        l.tx_off = (src + 4095) & ~4095ull;
-        l.rx_off = l.tx_off + pipes * l.pipe_stream;
-        const uint64_t bytes = l.rx_off + pipes * l.pipe_stream;
+        uint64_t at = (src + 4095) & ~4095ull;
+        l.slots.resize(depth);
+        for (Slot& S : l.slots) {  // per slot: the tunnel streams (sent, received)
+            S.tx_off = at;
+            S.rx_off = at + pipes * l.pipe_stream;
+            at = S.rx_off + pipes * l.pipe_stream;
+            S.size.resize((size_t)pipes * chunks);
+            S.len.resize(pipes);
+        }
+        const uint64_t bytes = at;
+        const uint64_t tx0 = l.slots[0].tx_off;
         l.mem = static_cast<uint8_t*>(aligned_alloc(4096, bytes));
         uint64_t x = 0xC1C10000ull + t;
         for (uint64_t i = 0; i + 8 <= src; i += 8) {
             const uint64_t v = splitmix(x);
             memcpy(l.mem + i, &v, 8);
         }
-        memset(l.mem + l.tx_off, 0, bytes - l.tx_off);
+        memset(l.mem + tx0, 0, bytes - tx0);
         if ((st = cyaes_batcher_register_pool(b, l.mem, bytes, &l.pool)) != CYAES_OK) {
             fprintf(stderr, "cyaes_batcher_register_pool: %s\n", cyaes_strerror(st));
             return 1;
@@ -283,10 +339,10 @@ int main(int argc, char** argv) {
     cyaes_batcher_destroy(b);
     for (auto& l : L) free(l.mem);
     printf("{\"metric\": \"relay packets/s through both ends (SEAL, tunnel stream, parse, OPEN), host to host\", "
-           "\"size\": \"%s\", \"threads\": %u, \"pipes_per_thread\": %u, \"chunks_per_pipe_round\": %u, "
+           "\"size\": \"%s\", \"threads\": %u, \"pipes_per_thread\": %u, \"chunks_per_pipe_round\": %u, \"depth\": %u, "
            "\"recv_copy\": %u, \"seconds\": %.2f, \"rounds\": %llu, \"packets\": %llu, \"packets_per_s\": %.0f, "
            "\"payload_gibs\": %.3f, \"verified\": %llu, \"mismatches\": %llu, \"error\": %d}\n",
-           size_arg.c_str(), threads, pipes, chunks, recv_copy, s, (unsigned long long)rounds,
+           size_arg.c_str(), threads, pipes, chunks, depth, recv_copy, s, (unsigned long long)rounds,
            (unsigned long long)packets, packets / s, payload / s / (1ull << 30), (unsigned long long)verified,
            (unsigned long long)mismatches, err ? err : fl);
     return (err || fl || mismatches) ? 2 : 0;
