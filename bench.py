@@ -746,9 +746,10 @@ def main():
 
     # Relay packet stream in HBM: config B's payloads at
     # packet offset 12 with a 12-B gap per packet (stride 1,484 B, 4-B aligned
-    # payloads, relay_local.cpp:189-206), encrypted then decrypted in place by the
-    # ragged kernels with the runtime's default kernel choice.  Reported beside
-    # the headline, never as `value`.
+    # payloads, relay_local.cpp:189-206), encrypted then decrypted in place with
+    # the runtime's default kernel choice, through the strided entry points (the
+    # payloads are equally strided) and, as `ragged`, the ragged ones.  Reported
+    # beside the headline, never as `value`.
     relay = None
     if args.relay_stream and "B" in CONFIGS:
         rn, rpb, _ = CONFIGS["B"]
@@ -763,54 +764,65 @@ def main():
         d_off = torch.arange(rn, dtype=torch.int64, device="cuda") * stride + hdr
         d_nb = torch.full((rn,), rpb, dtype=torch.int32, device="cuda")
 
-        def r_enc():
-            ctx.encrypt_ragged(buf, buf, d_off, d_nb, rn, stream=sh)
-
-        def r_dec():
-            ctx.decrypt_ragged(buf, buf, d_off, d_nb, rn, stream=sh)
-
-        rpar = None
-        if not args.no_verify:
-            r_enc()
-            ok = ctx.check() == ca.CYAES_OK
-            g = golden.get("B") if rank == 0 else None
-            if g and g["npayloads"] == rn and g["p0"] == p0:
-                ct = view[:, hdr:hdr + rpb].contiguous()
-                ok = ok and ["%016x" % v for v in ctx.digest(ct, rn * rpb, sh)] == g["cipher_digest"]
-                del ct
-            r_dec()
-            ok = ok and ctx.check() == ca.CYAES_OK and bool(torch.equal(view[:, hdr:hdr + rpb].reshape(-1), d_pt))
-            ok = ok and bool((view[:, :hdr] == 0xA5).all())
-            rpar = "bit-exact" if all_ok(ok) else "MISMATCH"
-        for _ in range(args.packet_warmup):
-            r_enc()
-            r_dec()
-        rev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-                torch.cuda.Event(enable_timing=True)) for _ in range(args.packet_steps)]
-        if dist_on:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(args.packet_steps):
-            rev[i][0].record(stream)
-            r_enc()
-            rev[i][1].record(stream)
-            r_dec()
-            rev[i][2].record(stream)
-        torch.cuda.synchronize()
-        if dist_on:
-            dist.barrier()
-        rt = max_over_ranks(time.perf_counter() - t0)
-        relay = {
-            "value": round(2.0 * rn * rpb * args.packet_steps * world / rt / gib, 2), "unit": "GiB/s",
-            "layout": "config B payloads (%d x %d B per GPU) at packet offset %d, packet stride %d B, in place"
-                      % (rn, rpb, hdr, stride),
-            "encrypt_ms": round(sum(a.elapsed_time(b) for a, b, _ in rev) / args.packet_steps, 4),
-            "decrypt_ms": round(sum(b.elapsed_time(c) for _, b, c in rev) / args.packet_steps, 4),
-            "steps": args.packet_steps, "warmup": args.packet_warmup, "parity": rpar,
-            "parity_note": "gathered ciphertext digest vs config B's OpenSSL digest (rank 0 shard); "
-                           "headers untouched; decrypt restores the plaintext",
+        # The receiver's integration: parse the stream (cyaes_relay_parse /
+        # cyaes_relay_payloads) and, when the payloads are equally strided, as a
+        # stream of MTU packets is, run the strided entry points; the ragged ones
+        # (device offset and size lists) otherwise.  Both are timed.
+        apis = {
+            "strided": (lambda: ctx.encrypt_strided(buf, buf, hdr, stride, rn, rpb, stream=sh),
+                        lambda: ctx.decrypt_strided(buf, buf, hdr, stride, rn, rpb, stream=sh)),
+            "ragged": (lambda: ctx.encrypt_ragged(buf, buf, d_off, d_nb, rn, stream=sh),
+                       lambda: ctx.decrypt_ragged(buf, buf, d_off, d_nb, rn, stream=sh)),
         }
+        relay = {}
+        for api, (r_enc, r_dec) in apis.items():
+            rpar = None
+            if not args.no_verify:
+                view[:, hdr:hdr + rpb] = d_pt.view(rn, rpb)
+                r_enc()
+                ok = ctx.check() == ca.CYAES_OK
+                g = golden.get("B") if rank == 0 else None
+                if g and g["npayloads"] == rn and g["p0"] == p0:
+                    ct = view[:, hdr:hdr + rpb].contiguous()
+                    ok = ok and ["%016x" % v for v in ctx.digest(ct, rn * rpb, sh)] == g["cipher_digest"]
+                    del ct
+                r_dec()
+                ok = ok and ctx.check() == ca.CYAES_OK and bool(torch.equal(view[:, hdr:hdr + rpb].reshape(-1), d_pt))
+                ok = ok and bool((view[:, :hdr] == 0xA5).all())
+                rpar = "bit-exact" if all_ok(ok) else "MISMATCH"
+            for _ in range(args.packet_warmup):
+                r_enc()
+                r_dec()
+            rev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+                    torch.cuda.Event(enable_timing=True)) for _ in range(args.packet_steps)]
+            if dist_on:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(args.packet_steps):
+                rev[i][0].record(stream)
+                r_enc()
+                rev[i][1].record(stream)
+                r_dec()
+                rev[i][2].record(stream)
+            torch.cuda.synchronize()
+            if dist_on:
+                dist.barrier()
+            rt = max_over_ranks(time.perf_counter() - t0)
+            relay[api] = {
+                "value": round(2.0 * rn * rpb * args.packet_steps * world / rt / gib, 2), "unit": "GiB/s",
+                "encrypt_ms": round(sum(a.elapsed_time(b) for a, b, _ in rev) / args.packet_steps, 4),
+                "decrypt_ms": round(sum(b.elapsed_time(c) for _, b, c in rev) / args.packet_steps, 4),
+                "parity": rpar,
+            }
+        relay = dict(relay["strided"], ragged=relay["ragged"], api="cyaes_gpu_{en,de}crypt_strided "
+                     "(cyaes_relay_stride finds the stream equally strided); `ragged`: the same stream through "
+                     "cyaes_gpu_{en,de}crypt_ragged with device offset / size lists",
+                     layout="config B payloads (%d x %d B per GPU) at packet offset %d, packet stride %d B, in place"
+                            % (rn, rpb, hdr, stride),
+                     steps=args.packet_steps, warmup=args.packet_warmup,
+                     parity_note="gathered ciphertext digest vs config B's OpenSSL digest (rank 0 shard); "
+                                 "headers untouched; decrypt restores the plaintext")
         del buf, view, d_pt, d_off, d_nb
         torch.cuda.empty_cache()
 

@@ -76,6 +76,10 @@ _SIGS = {
                                                 _vp, _vp, _vp]),
     "cyaes_gpu_decrypt_ragged": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32,
                                                 _vp, _vp, _vp]),
+    "cyaes_gpu_encrypt_strided": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                 ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
+    "cyaes_gpu_decrypt_strided": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                 ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
     "cyaes_gpu_check": (ctypes.c_int, [_vp]),
     "cyaes_gpu_check_stream": (ctypes.c_int, [_vp, _vp]),
     "cyaes_gpu_encrypt_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
@@ -95,6 +99,7 @@ _SIGS = {
     "cyaes_relay_parse": (ctypes.c_uint32, [_vp, ctypes.c_size_t, _vp, _vp, _vp, ctypes.c_uint32,
                                             ctypes.POINTER(ctypes.c_size_t)]),
     "cyaes_relay_payloads": (ctypes.c_int64, [_vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint64, _vp, _vp]),
+    "cyaes_relay_stride": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
     "cyaes_relay_forward_id": (ctypes.c_int32, [_vp]),
     "cyaes_relay_forward_size": (ctypes.c_int32, [_vp]),
     # include/cyaes_adler32.h
@@ -339,6 +344,20 @@ class GpuContext:
                                                   _p(key_idx), payloads_per_key, _p(iv_in), _p(iv_out),
                                                   _p(stream)), "decrypt_ragged")
 
+    def encrypt_strided(self, d_in, d_out, first_offset, stride, npayloads, payload_bytes, key_idx=None,
+                        payloads_per_key=0, stream=None):
+        """Payload p at byte first_offset + p * stride (cyaes_gpu_encrypt_strided)."""
+        _check(self._lib.cyaes_gpu_encrypt_strided(self._h, _p(d_in), _p(d_out), first_offset, stride, npayloads,
+                                                   payload_bytes, _p(key_idx), payloads_per_key, _p(stream)),
+               "encrypt_strided")
+
+    def decrypt_strided(self, d_in, d_out, first_offset, stride, npayloads, payload_bytes, key_idx=None,
+                        payloads_per_key=0, stream=None):
+        """Payload p at byte first_offset + p * stride (cyaes_gpu_decrypt_strided)."""
+        _check(self._lib.cyaes_gpu_decrypt_strided(self._h, _p(d_in), _p(d_out), first_offset, stride, npayloads,
+                                                   payload_bytes, _p(key_idx), payloads_per_key, _p(stream)),
+               "decrypt_strided")
+
     def encrypt_host(self, h_in, h_out, npayloads, payload_bytes, payloads_per_key=0, chunk_bytes=0):
         """Host-resident batch (host addresses or CPU tensors), PCIe-inclusive; synchronous."""
         _check(self._lib.cyaes_gpu_encrypt_host(self._h, _p(h_in), _p(h_out), npayloads, payload_bytes,
@@ -420,6 +439,19 @@ def relay_payloads(packets, base=0):
     if j < 0:
         raise ValueError("RELAY_FORWARD packet with a payload that is not a multiple of 16")
     return list(po[:j]), list(pl[:j])
+
+
+def relay_stride(pay_off, pay_len):
+    """(first, stride, payload_bytes) if the payloads are equally strided and sized
+    (cyaes_relay_stride; for cyaes_gpu_*_strided), else None."""
+    lib = load_library()
+    n = len(pay_off)
+    off = (ctypes.c_uint64 * max(1, n))(*pay_off)
+    ln = (ctypes.c_uint32 * max(1, n))(*pay_len)
+    first, stride, pb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint32()
+    if not lib.cyaes_relay_stride(off, ln, n, ctypes.byref(first), ctypes.byref(stride), ctypes.byref(pb)):
+        return None
+    return first.value, stride.value, pb.value
 
 
 # ---- asynchronous batching adapter (include/cyaes_batch.h) ------------------

@@ -39,16 +39,73 @@ __device__ __forceinline__ void flat_position(const DecArgs& a, FlatPos ps, uint
     }
 }
 
+// STRIDED batches (a relay stream of equal packets resident in HBM): payload p
+// lies at byte off0 + p * stride (4-B aligned), so block r of payload p is at
+// off0 + p * stride + 16 r; the flat block order, chaining and rows are the
+// same as a contiguous batch's, only the addresses differ.
+__device__ __forceinline__ uint64_t soff(const DecArgs& a, uint64_t p, uint32_t r) {
+    return a.off0 + p * a.stride + 16ull * r;
+}
+// The same without off0 (folded into the range's base pointers) for 32-bit
+// payload indices: one v_mad_u64_u32 per row.
+__device__ __forceinline__ uint64_t soff32(uint32_t stride, uint32_t p, uint32_t r) {
+    return (uint64_t)p * stride + 16u * r;
+}
+__device__ __forceinline__ uint64_t soff_g(const DecArgs& a, uint64_t g) {  // flat block g (partial steps only)
+    const uint64_t p = g / a.bpp.d;
+    return soff(a, p, (uint32_t)(g - p * a.bpp.d));
+}
+__device__ __forceinline__ Ext data_ext(const uint8_t* base, const DecArgs& a, bool strided) {
+    return strided ? ext(base + a.off0, (a.npayloads - 1) * a.stride + 16ull * a.bpp.d) : ext(base, 16 * a.nblocks);
+}
+// Position (r, p) of row k's block in a STRIDED !BIG full step, from row 0's
+// (rk[0], pk[0]): rows are 64 blocks apart and payloads >= 64 blocks (the
+// runtime's condition for STRIDED), so each row wraps at most once.  Only row
+// 0's position is carried across steps: two VGPRs, where tracking every row
+// took eight and the step loop lost its schedule at the 128-VGPR limit.
+__device__ __forceinline__ void srow_pos(uint32_t bpp, int k, const uint32_t (&rk)[kDecRows],
+                                         const uint32_t (&pk)[kDecRows], uint32_t& r, uint32_t& p) {
+    r = rk[0];
+    p = pk[0];
+    for (int j = 0; j < k; j++) {
+        const uint32_t t = r + 64;
+        const bool wrap = t >= bpp;
+        r = wrap ? t - bpp : t;
+        p += wrap ? 1u : 0u;
+    }
+}
+// Byte offset (from in + off0) of row k's block in a STRIDED full step: !BIG
+// from row 0's tracked position, BIG from the step position (at most one
+// payload start).
+template <bool BIG>
+__device__ __forceinline__ uint64_t srow(const DecArgs& a, FlatPos ps, uint32_t lane, int k, const uint32_t (&rk)[kDecRows],
+                                         const uint32_t (&pk)[kDecRows]) {
+    const uint32_t stride = (uint32_t)a.stride;  // (the runtime keeps strides and payload indices 32-bit)
+    if (BIG) {
+        const uint32_t lpos = ps.bpos + 64 * k + lane;
+        const bool next = lpos >= a.bpp.d;
+        return soff32(stride, (uint32_t)ps.bp + (next ? 1u : 0u), next ? lpos - a.bpp.d : lpos);
+    }
+    uint32_t r, p;
+    srow_pos(a.bpp.d, k, rk, pk, r, p);
+    return soff32(stride, p, r);
+}
+
 // Loads the R rows of the step at `base` (c); partial steps also load each
 // block's predecessor (pv), full steps take it from the neighbour lane.
 // FULL: all 64*R blocks are in range (every step but possibly the batch's
-// last), so loads are unguarded and use immediate offsets off one lane pointer.
-template <bool FULL>
-__device__ __forceinline__ void flat_load(const DecArgs& a, uint32_t lane, uint64_t base, uint64_t end,
-                                          uint4 (&c)[kDecRows], uint4 (&pv)[kDecRows]) {
+// last), so loads are unguarded and use immediate offsets off one lane pointer
+// (STRIDED: one address per row).
+template <bool FULL, bool BIG, bool STRIDED>
+__device__ __forceinline__ void flat_load(const DecArgs& a, const uint8_t* in_s, uint32_t lane, uint64_t base,
+                                          uint64_t end, FlatPos ps, const uint32_t (&rk)[kDecRows],
+                                          const uint32_t (&pk)[kDecRows], uint4 (&c)[kDecRows], uint4 (&pv)[kDecRows]) {
     constexpr int R = kDecRows;
-    const Ext ie = ext(a.in, 16 * a.nblocks);
-    if (FULL) {
+    const Ext ie = data_ext(a.in, a, STRIDED);
+    if (FULL && STRIDED) {  // in_s = in + off0
+#pragma unroll
+        for (int k = 0; k < R; k++) c[k] = LD16U(in_s + srow<BIG>(a, ps, lane, k, rk, pk), ie);
+    } else if (FULL) {
         const uint8_t* g0 = a.in + 16 * (base + lane);
 #pragma unroll
         for (int k = 0; k < R; k++) c[k] = LD16(g0 + 1024 * k, ie);
@@ -57,25 +114,32 @@ __device__ __forceinline__ void flat_load(const DecArgs& a, uint32_t lane, uint6
 #pragma unroll
         for (int k = 0; k < R; k++) {
             const uint64_t g = min(base + 64 * k + lane, end - 1);
-            c[k] = LD16(a.in + 16 * g, ie);
             // The predecessor of block g (lane 0 of row 0 reads its own block:
             // the carry replaces it).  Block 0 has none: a 1-block batch (end
             // == 1) clamps every lane to g = 0, and g - 1 would read 16 B before
             // the buffer (r02 fault hunt, VERDICT r02 "What's weak" 1).  Block
             // 0 is a payload start, so its pv is the IV in flat_step anyway.
             const uint64_t back = (k == 0 && lane == 0) ? 0u : 1u;
-            pv[k] = LD16(a.in + 16 * (g >= back ? g - back : 0u), ie);
+            const uint64_t gp = g >= back ? g - back : 0u;
+            if (STRIDED) {
+                c[k] = LD16U(a.in + soff_g(a, g), ie);
+                pv[k] = LD16U(a.in + soff_g(a, gp), ie);
+            } else {
+                c[k] = LD16(a.in + 16 * g, ie);
+                pv[k] = LD16(a.in + 16 * gp, ie);
+            }
         }
     }
 }
 
-template <bool KEYED, bool BIG, bool FULL, bool IV>
+template <bool KEYED, bool BIG, bool FULL, bool IV, bool STRIDED>
 __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, uint32_t lo, uint32_t lane,
                                            uint64_t base, uint64_t end, FlatPos ps, uint4 carry,
                                            uint32_t (&dk0)[44], uint32_t& dk_id, const uint4 (&c)[kDecRows],
-                                           uint4 (&pv)[kDecRows], const uint32_t (&rk)[kDecRows]) {
+                                           uint4 (&pv)[kDecRows], const uint32_t (&rk)[kDecRows],
+                                           const uint32_t (&pk)[kDecRows], uint8_t* out_s) {
     constexpr int R = kDecRows;
-    const Ext oe = ext(a.out, 16 * a.nblocks);
+    const Ext oe = data_ext(a.out, a, STRIDED);
     const Ext iv_in_e = iv_ext(a.iv_in, a.npayloads), iv_out_e = iv_ext(a.iv_out, a.npayloads);
     if (FULL) {
         // Predecessor blocks from the neighbour lane (DPP wave_shr:1), lane 0's
@@ -106,8 +170,11 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
         }
     } else if (!IV || !a.iv_in) {  // chains restart at DefaultIV: a select on the lane's tracked position
 #pragma unroll
-        for (int k = 0; k < R; k++)
-            if (rk[k] == 0) pv[k] = default_iv();
+        for (int k = 0; k < R; k++) {
+            uint32_t r = rk[k], p;
+            if (STRIDED) srow_pos(a.bpp.d, k, rk, pk, r, p);
+            if (r == 0) pv[k] = default_iv();
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < R; k++) {
@@ -183,14 +250,22 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
             }
         }
     }
-    if (FULL) {
+    if (FULL && STRIDED) {
+#pragma unroll
+        for (int k = 0; k < R; k++) ST16U(out_s + srow<BIG>(a, ps, lane, k, rk, pk), oe, d[k]);
+    } else if (FULL) {
         uint8_t* o0 = a.out + 16 * (base + lane);
 #pragma unroll
         for (int k = 0; k < R; k++) ST16(o0 + 1024 * k, oe, d[k]);
     } else {
 #pragma unroll
-        for (int k = 0; k < R; k++)
-            if (base + 64 * k + lane < end) ST16(a.out + 16 * (base + 64 * k + lane), oe, d[k]);
+        for (int k = 0; k < R; k++) {
+            const uint64_t g = base + 64 * k + lane;
+            if (g < end) {
+                if (STRIDED) ST16U(a.out + soff_g(a, g), oe, d[k]);
+                else ST16(a.out + 16 * g, oe, d[k]);
+            }
+        }
     }
     return make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));  // next carry
 }
@@ -204,7 +279,7 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
 // nullptr); the IV code and the payload-index tracking compile out, which
 // keeps the SGPR budget of the round loop (with them, the !BIG SESS kernel
 // scheduled its rounds with 321 s_waitcnt per 640 LDS reads against 173).
-template <bool KEYED, bool BIG, bool SESS, bool IV>
+template <bool KEYED, bool BIG, bool SESS, bool IV, bool STRIDED>
 __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     constexpr int R = kDecRows;
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
@@ -246,9 +321,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
         ps.bp = begin / a.bpp.d;
         ps.bpos = (uint32_t)(begin - ps.bp * a.bpp.d);
         uint4 carry = make_uint4(0, 0, 0, 0);  // C[begin-1]
-        if (ps.bpos != 0)  // (begin >= 1 here)
-            carry = ka->boundary ? LD16(ka->boundary + ticket, ext(ka->boundary, 16ull * ka->nranges))
-                                 : LD16(ka->in + 16 * (begin - 1), ext(ka->in, 16 * ka->nblocks));
+        if (ps.bpos != 0) {  // (begin >= 1 here)
+            if (ka->boundary) carry = LD16(ka->boundary + ticket, ext(ka->boundary, 16ull * ka->nranges));
+            else if (STRIDED) carry = LD16U(a.in + soff(a, ps.bp, ps.bpos - 1), data_ext(a.in, a, true));
+            else carry = LD16(ka->in + 16 * (begin - 1), ext(ka->in, 16 * ka->nblocks));
+        }
         // SESS: a range lies in one session (the runtime makes range_blocks
         // divide sess_blocks); its schedule is loaded per range (11 loads per
         // range: tracking the current session kept one more SGPR live and the
@@ -256,38 +333,58 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
         if (SESS) load_sched(a.keys, (uint32_t)(begin / ka->sess_blocks), 1, dk0);
         // !BIG: each lane tracks its rows' positions in their payloads, advanced
         // by step_r per step (one add and a min instead of a division per row).
-        uint32_t rk[R];
+        // STRIDED: row 0's position and payload only (srow_pos derives the rest)
+        uint32_t rk[R], pk[R];
         if (!BIG) {
 #pragma unroll
-            for (int k = 0; k < R; k++) {
+            for (int k = 0; k < (STRIDED ? 1 : R); k++) {
                 const uint32_t lpos = ps.bpos + 64 * k + lane;
                 const Fastdiv bd = {ka->bpp.M, ka->bpp.d};
-                rk[k] = lpos - fastdiv(lpos, bd) * bd.d;
+                const uint32_t q = fastdiv(lpos, bd);
+                rk[k] = lpos - q * bd.d;
+                if (STRIDED) pk[k] = (uint32_t)ps.bp + q;
             }
         }
-        uint64_t base = begin;
-        uint4 c[R], pv[R];
-        if (base + 64 * R <= end) flat_load<true>(a, lane, base, end, c, pv);
-        for (; base + 64 * R <= end; base += 64 * R) {
-            // (Issuing the next step's loads before this step's rounds measured ~1 %
-            // slower: the LDS binds, and the other 15 waves hide the loads.)
-            carry = flat_step<KEYED, BIG, true, IV>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv, rk);
-            if (base + 128 * R <= end) flat_load<true>(a, lane, base + 64 * R, end, c, pv);
-            prio_feedback(leadp, ++prog, kDecPrioDiv);
+        auto advance = [&] {
             ps.bpos += a.step_r;
             ps.bp += a.step_q;
             if (ps.bpos >= a.bpp.d) { ps.bpos -= a.bpp.d; ps.bp++; }
             if (!BIG) {
 #pragma unroll
-                for (int k = 0; k < R; k++) {
+                for (int k = 0; k < (STRIDED ? 1 : R); k++) {
                     const uint32_t t = rk[k] + a.step_r;  // < 2 bpp
+                    if (STRIDED) pk[k] += a.step_q + (t >= a.bpp.d ? 1u : 0u);
                     rk[k] = min(t, t - a.bpp.d);
                 }
             }
+        };
+        // STRIDED: the range's base pointers with off0 folded in (kernel arguments, re-read per range)
+        const uint8_t* in_s = STRIDED ? ka->in + ka->off0 : nullptr;
+        uint8_t* out_s = STRIDED ? ka->out + ka->off0 : nullptr;
+        uint64_t base = begin;
+        uint4 c[R], pv[R];
+        if (base + 64 * R <= end) flat_load<true, BIG, STRIDED>(a, in_s, lane, base, end, ps, rk, pk, c, pv);
+        for (; base + 64 * R <= end; base += 64 * R) {
+            // (Issuing the next step's loads before this step's rounds measured ~1 %
+            // slower: the LDS binds, and the other 15 waves hide the loads.)
+            carry = flat_step<KEYED, BIG, true, IV, STRIDED>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv,
+                                                             rk, pk, out_s);
+            if (STRIDED) {  // the next step's addresses come from its positions
+                advance();
+                if (base + 128 * R <= end)
+                    flat_load<true, BIG, STRIDED>(a, in_s, lane, base + 64 * R, end, ps, rk, pk, c, pv);
+                prio_feedback(leadp, ++prog, kDecPrioDiv);
+            } else {
+                if (base + 128 * R <= end)
+                    flat_load<true, BIG, STRIDED>(a, in_s, lane, base + 64 * R, end, ps, rk, pk, c, pv);
+                prio_feedback(leadp, ++prog, kDecPrioDiv);
+                advance();
+            }
         }
         if (base < end) {  // the batch's last, partial step (only the last range has one)
-            flat_load<false>(a, lane, base, end, c, pv);
-            flat_step<KEYED, BIG, false, IV>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv, rk);
+            flat_load<false, BIG, STRIDED>(a, in_s, lane, base, end, ps, rk, pk, c, pv);
+            flat_step<KEYED, BIG, false, IV, STRIDED>(a, lds, lo, lane, base, end, ps, carry, dk0, dk_id, c, pv, rk, pk,
+                                                      out_s);
         }
         if (KEYED || IV) break;
         ticket = ka->dyn ? next_ticket(ka->work) : ticket + nwaves;
@@ -297,15 +394,16 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
 // Before a decrypt (one small launch, stream-ordered): zero the launch's work
 // words, and for an in-place flat decrypt snapshot C[begin-1] of every range
 // before any wave overwrites it.
-__global__ void k_dec_prepass(const uint4* in, uint64_t nblocks, uint64_t range_blocks, uint64_t nranges,
-                              Fastdiv bpp, uint4* boundary, uint32_t* work, uint32_t work_words) {
+__global__ void k_dec_prepass(DecArgs a, uint32_t work_words) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < work_words) work[r] = 0;
-    if (!boundary || r >= nranges) return;
-    const uint64_t begin = r * range_blocks;
-    if (begin == 0 || begin >= nblocks) return;
-    if (begin % bpp.d != 0)
-        ST16(boundary + r, ext(boundary, 16 * nranges), LD16(in + (begin - 1), ext(in, 16 * nblocks)));
+    if (r < work_words) a.work[r] = 0;
+    if (!a.boundary || r >= a.nranges) return;
+    const uint64_t begin = r * a.range_blocks;
+    if (begin == 0 || begin >= a.nblocks || begin % a.bpp.d == 0) return;
+    uint4* snap = const_cast<uint4*>(a.boundary) + r;
+    const Ext se = ext(a.boundary, 16 * a.nranges);
+    if (a.stride) ST16(snap, se, LD16U(a.in + soff_g(a, begin - 1), data_ext(a.in, a, true)));
+    else ST16(snap, se, LD16(a.in + 16 * (begin - 1), ext(a.in, 16 * a.nblocks)));
 }
 
 }  // namespace
@@ -316,14 +414,17 @@ hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream) {
     const dim3 g(grid), b(kDecThreads);
     const bool sess = a.sess_blocks != 0;  // keyed by step-aligned sessions: the unkeyed step per session
     const bool iv = a.iv_in != nullptr || a.iv_out != nullptr;  // (the runtime sets sess only without IVs)
-    if (sess && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, true, false>), g, b, 0, stream, a);
-    else if (sess) hipLaunchKernelGGL((k_decrypt_flat<false, false, true, false>), g, b, 0, stream, a);
-    else if (keyed && big) hipLaunchKernelGGL((k_decrypt_flat<true, true, false, true>), g, b, 0, stream, a);
-    else if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true, false, false, true>), g, b, 0, stream, a);
-    else if (big && iv) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, true>), g, b, 0, stream, a);
-    else if (big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false>), g, b, 0, stream, a);
-    else if (iv) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, true>), g, b, 0, stream, a);
-    else hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false>), g, b, 0, stream, a);
+    // STRIDED: unkeyed, no IV arrays (the runtime checks)
+    if (a.stride && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false, true>), g, b, 0, stream, a);
+    else if (a.stride) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false, true>), g, b, 0, stream, a);
+    else if (sess && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, true, false, false>), g, b, 0, stream, a);
+    else if (sess) hipLaunchKernelGGL((k_decrypt_flat<false, false, true, false, false>), g, b, 0, stream, a);
+    else if (keyed && big) hipLaunchKernelGGL((k_decrypt_flat<true, true, false, true, false>), g, b, 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true, false, false, true, false>), g, b, 0, stream, a);
+    else if (big && iv) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, true, false>), g, b, 0, stream, a);
+    else if (big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false, false>), g, b, 0, stream, a);
+    else if (iv) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, true, false>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false, false>), g, b, 0, stream, a);
     return hipGetLastError();
 }
 
@@ -331,8 +432,7 @@ hipError_t launch_dec_prepass(const DecArgs& a, uint32_t work_words, hipStream_t
     const int threads = 256;
     const uint64_t n = std::max<uint64_t>(work_words, a.boundary ? a.nranges : 0);
     const int grid = (int)((n + threads - 1) / threads);
-    hipLaunchKernelGGL(k_dec_prepass, dim3(grid), dim3(threads), 0, stream, reinterpret_cast<const uint4*>(a.in),
-                       a.nblocks, a.range_blocks, a.nranges, a.bpp, const_cast<uint4*>(a.boundary), a.work, work_words);
+    hipLaunchKernelGGL(k_dec_prepass, dim3(grid), dim3(threads), 0, stream, a, work_words);
     return hipGetLastError();
 }
 
@@ -341,6 +441,7 @@ int bounds_read_dec(unsigned long long* rec4, unsigned int* lines) { return read
 #endif
 #if CYAES_CLOCK_PROBE
 int probe_read_dec(unsigned long long* out8) { return read_probe_local(out8); }
+int timeline_read_dec(int kind, uint4* out) { return read_timeline_local(kind, out); }
 #endif
 
 }  // namespace cyaes

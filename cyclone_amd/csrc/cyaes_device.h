@@ -369,6 +369,12 @@ __device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kI
 // body, summed per kernel kind into g_probe and read by cyaes_debug_probe()
 // (bench.py and tools/ab.py print the clock).
 __device__ unsigned long long g_probe[2][4];  // [enc, dec] x {cycles, ticks, waves, max ticks}
+// Per-wave timeline of the last launch of each kind (tools/timeline.py): wave
+// slot blockIdx.x * waves per block + wave: {start ticks, end ticks (low 32
+// bits of s_memrealtime), HW_ID, XCC_ID}, {cycles (s_memtime) low, high,
+// blockIdx.x, wave in block}.
+constexpr uint32_t kTimelineWaves = 8192;
+__device__ uint4 g_timeline[2][kTimelineWaves][2];
 struct ClockProbe {
     uint64_t t0, r0;
     int kind;
@@ -380,6 +386,14 @@ struct ClockProbe {
             atomicAdd(&g_probe[kind][1], (unsigned long long)(r1 - r0));
             atomicAdd(&g_probe[kind][2], 1ull);
             atomicMax(&g_probe[kind][3], (unsigned long long)(r1 - r0));
+            const uint32_t w = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+            if (w < kTimelineWaves) {
+                const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
+                const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+                g_timeline[kind][w][0] = make_uint4((uint32_t)r0, (uint32_t)r1, hw, xcc);
+                g_timeline[kind][w][1] = make_uint4((uint32_t)(t1 - t0), (uint32_t)((t1 - t0) >> 32), blockIdx.x,
+                                                    threadIdx.x >> 6);
+            }
         }
     }
 };
@@ -413,6 +427,12 @@ inline int read_bounds_local(unsigned long long* rec4, unsigned int* lines) {
 }
 #endif
 #if CYAES_CLOCK_PROBE
+inline int read_timeline_local(int kind, uint4* out) {  // kTimelineWaves x 2 records, then cleared
+    const size_t bytes = sizeof(uint4) * 2 * kTimelineWaves;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_timeline), bytes, bytes * kind) != hipSuccess) return -1;
+    static uint4 zero[2 * kTimelineWaves];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), zero, bytes, bytes * kind) == hipSuccess ? 0 : -1;
+}
 inline int read_probe_local(unsigned long long* out8) {
     if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_probe), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
     static const unsigned long long zero[8] = {};

@@ -293,6 +293,7 @@ int bounds_read_enc(unsigned long long* rec4, unsigned int* lines) { return read
 #endif
 #if CYAES_CLOCK_PROBE
 int probe_read_enc(unsigned long long* out8) { return read_probe_local(out8); }
+int timeline_read_enc(int kind, uint4* out) { return read_timeline_local(kind, out); }
 #endif
 
 }  // namespace cyaes

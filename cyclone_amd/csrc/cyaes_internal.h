@@ -126,6 +126,7 @@ struct DecArgs {
     uint32_t* status;
     uint32_t group;           // ragged kernel: payloads per wave group (1..64)
     uint64_t sess_blocks;     // flat kernel: blocks per payloads_per_key session when a multiple of a step, else 0
+    uint64_t off0, stride;    // flat kernel, stride != 0: payload p at byte off0 + p * stride (4-B aligned), else contiguous
 };
 
 // Launchers (cyaes_*kernels.hip).  All asynchronous on `stream`.
@@ -139,6 +140,8 @@ hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, int threads, hipStr
 hipError_t launch_dec_prepass(const DecArgs& a, uint32_t work_words, hipStream_t stream);
 hipError_t launch_key_expand(const uint8_t* d_keys, uint32_t nkeys, const uint8_t* d_sbox,
                              uint32_t* d_sched, hipStream_t stream);
+hipError_t launch_strided_lists(uint64_t* offsets, uint32_t* nbytes, uint64_t first, uint64_t stride, uint64_t n,
+                                uint32_t payload_bytes, hipStream_t stream);
 hipError_t launch_fill_synthetic(uint8_t* buf, uint64_t p0, uint64_t npayloads, uint32_t payload_bytes,
                                  uint64_t seed, hipStream_t stream);
 hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long* out2, hipStream_t stream);
@@ -149,6 +152,8 @@ int bounds_read_enc(unsigned long long* rec4, unsigned int* lines);
 int bounds_read_dec(unsigned long long* rec4, unsigned int* lines);
 int probe_read_enc(unsigned long long* out8);
 int probe_read_dec(unsigned long long* out8);
+int timeline_read_enc(int kind, uint4* out);
+int timeline_read_dec(int kind, uint4* out);
 
 // Batching adapter request descriptor (cyaes_batcher.cpp builds them in pinned
 // memory, cyaes_batch_kernels.hip reads them).  src / dst are DEVICE

@@ -205,6 +205,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     if (threadIdx.x == 0) *leadp = 0;
     uint32_t prog = 0;
     __syncthreads();
+    CLOCK_PROBE(1);
     const char* lds = reinterpret_cast<const char*>(lds_words);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lo = dec_lo(threadIdx.x);
@@ -509,6 +510,26 @@ hipError_t launch_key_expand(const uint8_t* d_keys, uint32_t nkeys, const uint8_
     return hipGetLastError();
 }
 
+// The ragged lists of a strided batch (cyaes_gpu_*_strided fallbacks):
+// offsets[p] = first + p * stride, nbytes[p] = payload_bytes.
+__global__ void k_strided_lists(uint64_t* offsets, uint32_t* nbytes, uint64_t first, uint64_t stride, uint64_t n,
+                                uint32_t payload_bytes) {
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (uint64_t)gridDim.x * blockDim.x) {
+        offsets[p] = first + p * stride;
+        nbytes[p] = payload_bytes;
+    }
+}
+
+hipError_t launch_strided_lists(uint64_t* offsets, uint32_t* nbytes, uint64_t first, uint64_t stride, uint64_t n,
+                                uint32_t payload_bytes, hipStream_t stream) {
+    const int threads = 256;
+    const uint64_t want = (n + threads - 1) / threads;
+    const int grid = (int)(want < 4096 ? (want ? want : 1) : 4096);
+    hipLaunchKernelGGL(k_strided_lists, dim3(grid), dim3(threads), 0, stream, offsets, nbytes, first, stride, n,
+                       payload_bytes);
+    return hipGetLastError();
+}
+
 hipError_t launch_fill_synthetic(uint8_t* buf, uint64_t p0, uint64_t npayloads, uint32_t payload_bytes, uint64_t seed,
                                  hipStream_t stream) {
     const int threads = 256;
@@ -542,6 +563,19 @@ extern "C" int cyaes_debug_probe(unsigned long long* out) {
         for (int t = 0; t < 3; t++) out[i] = (i % 4 == 3) ? std::max(out[i], part[t][i]) : out[i] + part[t][i];
     }
     return 0;
+}
+
+// Per-wave timeline of the last launch of a kind (0 encrypt, 1 decrypt) in one
+// kernel translation unit (0: this one -- quad encrypt, ragged decrypt; 1: the
+// lane encrypt; 2: the flat decrypt): kTimelineWaves x 2 uint4 (cyaes_device.h),
+// read and cleared.  tools/timeline.py.
+extern "C" int cyaes_debug_timeline(int tu, int kind, void* out) {
+    if (kind < 0 || kind > 1) return -1;
+    uint4* o = static_cast<uint4*>(out);
+    if (tu == 0) return cyaes::read_timeline_local(kind, o);
+    if (tu == 1) return cyaes::timeline_read_enc(kind, o);
+    if (tu == 2) return cyaes::timeline_read_dec(kind, o);
+    return -1;
 }
 #endif
 

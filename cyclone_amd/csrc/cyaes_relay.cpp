@@ -75,6 +75,19 @@ int64_t cyaes_relay_payloads(const uint64_t* offsets, const uint32_t* packet_siz
     return j;
 }
 
+int cyaes_relay_stride(const uint64_t* pay_off, const uint32_t* pay_len, uint64_t n, uint64_t* first, uint64_t* stride,
+                       uint32_t* payload_bytes) {
+    if (n == 0 || !pay_off || !pay_len || !first || !stride || !payload_bytes) return 0;
+    const uint64_t st = n > 1 ? pay_off[1] - pay_off[0] : pay_len[0];
+    if (n > 1 && (pay_off[1] < pay_off[0] || st < pay_len[0])) return 0;
+    for (uint64_t j = 0; j < n; j++)
+        if (pay_len[j] != pay_len[0] || pay_off[j] != pay_off[0] + j * st) return 0;
+    *first = pay_off[0];
+    *stride = st;
+    *payload_bytes = pay_len[0];
+    return 1;
+}
+
 int32_t cyaes_relay_forward_id(const uint8_t* pkt) { return pkt ? get_i32(pkt + CYAES_RELAY_HEADSIZE) : 0; }
 int32_t cyaes_relay_forward_size(const uint8_t* pkt) { return pkt ? get_i32(pkt + CYAES_RELAY_HEADSIZE + 4) : 0; }
 

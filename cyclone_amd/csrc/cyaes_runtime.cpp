@@ -28,6 +28,7 @@ struct cyaes_gpu {
     uint32_t dec_range_steps = kDecRangeSteps;  // env CYAES_DEC_RANGE_STEPS: steps per dynamic flat-decrypt range
     uint32_t dec_groups_per_wave = kDecGroupsPerWave;  // env CYAES_DEC_GROUPS_PER_WAVE: ragged groups per wave
     int dec_grid_max = 0;       // env CYAES_DEC_GRID: cap on decrypt workgroups (tests: many ranges per wave on small batches)
+    bool strided_lists = false; // env CYAES_STRIDED_LISTS=1: strided decrypts as ragged batches (tests, A/B)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
     uint32_t* d_keys = nullptr;    // nkeys * kSchedWords
     uint32_t nkeys = 0;
@@ -220,10 +221,15 @@ int alias_iv(cyaes_gpu* ctx, StreamScratch& sc, const uint8_t** iv_in, const uin
     return CYAES_OK;
 }
 
+// Uniform batch (off0 = stride = 0: contiguous), or a strided one (payload p at
+// byte off0 + p * stride; unkeyed, no IV arrays, >= 64 blocks per payload, 32-bit
+// payload indices and stride: the callers check).
 int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t npayloads, uint32_t payload_bytes,
                     const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream,
-                    const uint32_t* table = nullptr, uint32_t table_keys = 0) {
+                    const uint32_t* table = nullptr, uint32_t table_keys = 0, uint64_t off0 = 0, uint64_t stride = 0) {
     DecArgs a = {};
+    a.off0 = off0;
+    a.stride = stride;
     int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys, table, table_keys);
     if (st) return st;
     if ((iv_in || iv_out) && npayloads > 0xFFFFFFFFull) return CYAES_EINVAL;
@@ -411,6 +417,7 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* v = getenv("CYAES_DEC_RANGE_STEPS")) ctx->dec_range_steps = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_DEC_GROUPS_PER_WAVE")) ctx->dec_groups_per_wave = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_DEC_GRID")) ctx->dec_grid_max = atoi(v);
+    if (const char* v = getenv("CYAES_STRIDED_LISTS")) ctx->strided_lists = atoi(v) != 0;
     const HostTables& t = host_tables();
     uint8_t host[kTablesBytes];
     memcpy(host + kEncTableOff, t.enc, sizeof(t.enc));
@@ -617,6 +624,47 @@ int cyaes_gpu_cbc_decrypt_batch(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_
                                 uint32_t npayloads, void* stream) {
     return cyaes_gpu_decrypt_ragged(ctx, d_in, d_out, d_offsets, d_nbytes, npayloads, d_key_idx, 0, d_iv, nullptr,
                                     stream);
+}
+
+// Strided batches: the decrypt runs the flat kernel's STRIDED addressing when
+// it applies (unkeyed, >= 64 blocks per payload: the relay's MTU packets);
+// anything else, and every encrypt, runs as the ragged batch it is, with the
+// two lists written on the device first (12 B per payload).
+static int strided_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* in, uint8_t* out, uint64_t first,
+                         uint64_t stride, uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx,
+                         uint32_t ppk, hipStream_t stream) {
+    if (!ctx || payload_bytes % 16 || first % 4 || stride % 4 || stride < payload_bytes) return CYAES_EINVAL;
+    if (npayloads == 0 || payload_bytes == 0) return CYAES_OK;
+    if (!ragged_args_ok(ctx, in, out, nullptr, nullptr)) return CYAES_EINVAL;
+    if (npayloads - 1 > (UINT64_MAX - first - payload_bytes) / stride) return CYAES_EINVAL;
+    DeviceGuard g(ctx->device);
+    const uint32_t bpp = payload_bytes / 16;
+    if (decrypt && !key_idx && !ppk && bpp >= 64 && npayloads <= 0xFFFFFFFFull && stride <= 0xFFFFFFFFull &&
+        !ctx->strided_lists)
+        return decrypt_uniform(ctx, in, out, npayloads, payload_bytes, nullptr, 0, nullptr, nullptr, stream, nullptr, 0,
+                               first, stride);
+    StreamScratch lists;
+    int st = lists.get(ctx->pool, npayloads * 12, stream);
+    if (st) return st;
+    uint64_t* offs = static_cast<uint64_t*>(lists.p);
+    uint32_t* nb = reinterpret_cast<uint32_t*>(offs + npayloads);
+    CY_TRY(launch_strided_lists(offs, nb, first, stride, npayloads, payload_bytes, stream));
+    return decrypt ? decrypt_ragged(ctx, in, out, offs, nb, npayloads, key_idx, ppk, nullptr, nullptr, stream)
+                   : encrypt_common(ctx, in, out, offs, nb, npayloads, 0, key_idx, ppk, nullptr, nullptr, stream);
+}
+
+int cyaes_gpu_encrypt_strided(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, uint64_t first_offset,
+                              uint64_t stride, uint64_t npayloads, uint32_t payload_bytes, const uint32_t* d_key_idx,
+                              uint32_t payloads_per_key, void* stream) {
+    return strided_batch(ctx, false, d_in, d_out, first_offset, stride, npayloads, payload_bytes, d_key_idx,
+                         payloads_per_key, (hipStream_t)stream);
+}
+
+int cyaes_gpu_decrypt_strided(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, uint64_t first_offset,
+                              uint64_t stride, uint64_t npayloads, uint32_t payload_bytes, const uint32_t* d_key_idx,
+                              uint32_t payloads_per_key, void* stream) {
+    return strided_batch(ctx, true, d_in, d_out, first_offset, stride, npayloads, payload_bytes, d_key_idx,
+                         payloads_per_key, (hipStream_t)stream);
 }
 
 int cyaes_gpu_check(cyaes_gpu* ctx) {

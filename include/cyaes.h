@@ -125,6 +125,23 @@ int cyaes_gpu_decrypt_ragged(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out
                              const uint32_t* d_nbytes, uint64_t npayloads, const uint32_t* d_key_idx,
                              uint32_t payloads_per_key, const uint8_t* d_iv_in, uint8_t* d_iv_out, void* stream);
 
+/* Strided layout (a relay stream of equal packets resident in HBM):
+ *                 payload p occupies [first_offset + p*stride, + payload_bytes);
+ *                 first_offset, stride and d_in/d_out multiples of 4, stride >=
+ *                 payload_bytes; the bytes between payloads are not touched.
+ *                 The same result as a ragged batch with d_offsets[p] =
+ *                 first_offset + p*stride and d_nbytes[p] = payload_bytes, without
+ *                 the two lists: the relay server's received stream of MTU
+ *                 packets, payload at packet offset 12, stride = packet size
+ *                 (relay_server.cpp:329; cyaes_relay_stride finds it).  No IV
+ *                 arrays (the relay passes iv = nullptr). */
+int cyaes_gpu_encrypt_strided(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, uint64_t first_offset,
+                              uint64_t stride, uint64_t npayloads, uint32_t payload_bytes, const uint32_t* d_key_idx,
+                              uint32_t payloads_per_key, void* stream);
+int cyaes_gpu_decrypt_strided(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, uint64_t first_offset,
+                              uint64_t stride, uint64_t npayloads, uint32_t payload_bytes, const uint32_t* d_key_idx,
+                              uint32_t payloads_per_key, void* stream);
+
 /* The batch entry points of SURVEY.md §8(b), as ragged batches with one
  * input IV per payload (d_iv: 16 B per payload, NULL => DefaultIV), key
  * d_key_idx[p] (NULL => key 0) and no IV write-back. */

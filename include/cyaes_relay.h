@@ -70,6 +70,14 @@ uint32_t cyaes_relay_parse(const uint8_t* stream, size_t len, uint64_t* offsets,
 int64_t cyaes_relay_payloads(const uint64_t* offsets, const uint32_t* packet_sizes, const uint16_t* packet_ids,
                              uint32_t npackets, uint64_t base, uint64_t* pay_off, uint32_t* pay_len);
 
+/* 1 if the n payloads of a ragged description are equally strided and
+ * equally sized (pay_off[j] = pay_off[0] + j * stride, pay_len[j] = pay_len[0],
+ * stride >= pay_len[0]): a stream of equal packets, which
+ * cyaes_gpu_{en,de}crypt_strided processes without device lists; *first,
+ * *stride and *payload_bytes are set then.  0 otherwise (n == 0 included). */
+int cyaes_relay_stride(const uint64_t* pay_off, const uint32_t* pay_len, uint64_t n, uint64_t* first, uint64_t* stride,
+                       uint32_t* payload_bytes);
+
 /* RelayForwardMsg fields of a packet starting at pkt (host byte order). */
 int32_t cyaes_relay_forward_id(const uint8_t* pkt);
 int32_t cyaes_relay_forward_size(const uint8_t* pkt);

@@ -807,3 +807,57 @@ def test_pooled_open_range_and_unregister_flush(batcher):
     batcher.unregister_pool(pid)
     assert batcher.flush() == ca.CYAES_OK
     batcher.session_close(slot)
+
+
+@pytest.mark.parametrize("chunk", [1456, 1024 - 8, 65272, 488])  # payloads of 92, 64, 4080 and 31 blocks
+@pytest.mark.parametrize("mode", ["default", "dyn1", "lists"])
+def test_device_relay_stream_strided(chunk, mode):
+    """A received stream of equal relay packets resident in HBM (the server's
+    tunnel buffer under bulk transfer): cyaes_relay_stride recognises the
+    payloads as equally strided (packet offset 12, stride = packet size) and
+    cyaes_gpu_{en,de}crypt_strided process them where they lie, in place and
+    out of place, headers untouched -- the flat kernel's strided addressing
+    for payloads of >= 64 blocks, the ragged kernels otherwise ("lists" forces
+    those), bit-exact against the relay restatement (relay_local.cpp:189-206,
+    relay_server.cpp:329)."""
+    import numpy as np
+    import torch
+    env = {"default": {}, "dyn1": {"CYAES_DEC_GRID": "3", "CYAES_DEC_RANGE_STEPS": "1"},
+           "lists": {"CYAES_STRIDED_LISTS": "1"}}[mode]
+    key = _keys(1, 51)[0]
+    rng = random.Random(51)
+    n = 700 if chunk < 60000 else 40
+    chunks = [bytes(rng.randrange(256) for _ in range(chunk)) for _ in range(n)]
+    plain = b"".join(ro.seal_forward(None, i, c, encrypt=False) for i, c in enumerate(chunks))
+    sealed = b"".join(ro.seal_forward(key, i, c) for i, c in enumerate(chunks))
+    parsed, used = ca.relay_parse(plain)
+    assert used == len(plain)
+    off, ln = ca.relay_payloads(parsed)
+    first, stride, pb = ca.relay_stride(off, ln)
+    assert (first, stride, pb) == (12, ca.relay_packet_bytes(chunk), ln[0])
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    ctx = ca.GpuContext(0)
+    for k, v in old.items():
+        os.environ.pop(k) if v is None else os.environ.__setitem__(k, v)
+    ctx.set_keys(key)
+    dev = torch.frombuffer(bytearray(plain), dtype=torch.uint8).cuda()
+    ctx.encrypt_strided(dev, dev, first, stride, n, pb)
+    assert bytes(dev.cpu().numpy().tobytes()) == sealed
+    ctx.decrypt_strided(dev, dev, first, stride, n, pb)
+    assert bytes(dev.cpu().numpy().tobytes()) == plain
+    # out of place: the bytes between payloads of the output stream are left alone
+    src = torch.frombuffer(bytearray(sealed), dtype=torch.uint8).cuda()
+    out = torch.full_like(src, 0x5A)
+    ctx.decrypt_strided(src, out, first, stride, n, pb)
+    got = out.cpu().numpy().tobytes()
+    want = bytearray(b"\x5a" * len(sealed))
+    for o in off:
+        want[o:o + pb] = plain[o:o + pb]
+    assert got == bytes(want)
+    assert ctx.check() == ca.CYAES_OK
+    # an irregular stream is not strided
+    assert ca.relay_stride(off[:-1] + [off[-1] + 4], ln) is None
+    with pytest.raises(ca.CyaesError):  # stride shorter than the payload
+        ctx.decrypt_strided(dev, dev, first, pb - 16, n, pb)
+    ctx.close()

@@ -184,6 +184,7 @@ def test_bench_line_contract_single_gpu():
     assert b["parity"] == "bit-exact" and b["payload_bytes"] == 1472 and b["cpu_baseline"]["matches_gpu"] is True
     r = out["relay_stream"]  # config B's payloads as an in-place relay packet stream, vs config B's digest
     assert r["parity"] == "bit-exact" and r["value"] > 0 and r["encrypt_ms"] > 0 and r["decrypt_ms"] > 0
+    assert r["ragged"]["parity"] == "bit-exact" and r["ragged"]["decrypt_ms"] > 0
     e = out["e2e"]  # host -> device -> host over pinned memory, beside the same run's link ceiling
     assert e["bit_exact"] is True and e["payloads"] == 4096 and e["enc_plus_dec"] > 0
     assert e["link"]["duplex_gibs_per_direction"] > 0 and 0 < e["frac_of_duplex_link"] < 1.5
@@ -217,4 +218,4 @@ def test_rccl_path_world_one_bit_exact():
     assert d["distinct_devices"] == 1 and d["same_keys_all_ranks"] is True
     assert out["shards"][0]["device"] == 0 and out["shards"][0]["pci"]
     assert out["packet_configs"]["D"]["parity"] == "bit-exact"
-    assert out["relay_stream"]["parity"] == "bit-exact"
+    assert out["relay_stream"]["parity"] == "bit-exact" and out["relay_stream"]["ragged"]["parity"] == "bit-exact"

@@ -134,6 +134,22 @@ def test_payloads_select_forward_packets():
         ca.relay_payloads(bad)
 
 
+def test_relay_stride_recognises_equal_packet_streams():
+    """cyaes_relay_stride: a parsed stream of equal FORWARD packets is one
+    strided batch (payload at packet offset 12, stride = packet size, the
+    layout cyaes_gpu_*_strided take); anything irregular is not."""
+    chunks = [bytes([i % 251]) * 1472 for i in range(50)]
+    stream = b"".join(ro.seal_forward(None, i, c, encrypt=False) for i, c in enumerate(chunks))
+    off, ln = ca.relay_payloads(ca.relay_parse(stream)[0], base=1000)
+    assert ca.relay_stride(off, ln) == (1012, ca.relay_packet_bytes(1472), 1472)
+    assert ca.relay_stride(off[:1], ln[:1]) == (1012, 1472, 1472)  # one payload: stride = its size
+    assert ca.relay_stride([], []) is None
+    assert ca.relay_stride(off, ln[:-1] + [1456]) is None             # a shorter last payload
+    assert ca.relay_stride(off[:10] + off[11:], ln[:-1]) is None      # a missing packet
+    assert ca.relay_stride([0, 100], [1472, 1472]) is None            # overlapping payloads
+    assert ca.relay_stride([100, 0], [16, 16]) is None                # descending offsets
+
+
 def test_batcher_without_device_fails_loudly():
     try:
         import torch

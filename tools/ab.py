@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--ppk", type=int, default=0, help="payloads per session key (0: one key)")
     ap.add_argument("--key-idx", action="store_true", help="with --ppk: the same sessions as a per-payload index array")
     ap.add_argument("--relay", action="store_true", help="relay packet stream in place (ragged kernels)")
+    ap.add_argument("--relay-api", default="ragged", choices=["ragged", "strided"],
+                    help="--relay: the ragged entry points (device lists) or the strided ones")
     args = ap.parse_args()
     import torch
     import cyclone_amd as ca
@@ -116,12 +118,18 @@ def relay(args, ctxs, pt, torch, s):
             view[:, hdr:hdr + pb] = pt.view(n, pb)
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record(s)
-            c.encrypt_ragged(buf, buf, d_off, d_nb, n, stream=s.cuda_stream)
+            if args.relay_api == "strided":
+                c.encrypt_strided(buf, buf, hdr, stride, n, pb, stream=s.cuda_stream)
+            else:
+                c.encrypt_ragged(buf, buf, d_off, d_nb, n, stream=s.cuda_stream)
             e[1].record(s)
             if r == 0:
                 torch.cuda.synchronize()
                 dct = c.digest(buf, n * stride)
-            c.decrypt_ragged(buf, buf, d_off, d_nb, n, stream=s.cuda_stream)
+            if args.relay_api == "strided":
+                c.decrypt_strided(buf, buf, hdr, stride, n, pb, stream=s.cuda_stream)
+            else:
+                c.decrypt_ragged(buf, buf, d_off, d_nb, n, stream=s.cuda_stream)
             e[2].record(s)
             torch.cuda.synchronize()
             if r == 0:

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""tools/ab_relay_layout.py -- where ragged encrypt loses time on relay streams.
+"""tools/ab_relay_layout.py -- where ragged encrypt and decrypt lose time on relay streams.
 
-Times cyaes_gpu_encrypt_ragged on N equal payloads under layouts that differ in
+Times cyaes_gpu_encrypt_ragged, then cyaes_gpu_decrypt_ragged of its output
+(in place, or back into the source stream), on N equal payloads under layouts that differ in
 one property at a time: packet stride (payload + header bytes), payload offset
 inside the packet (12 = relay, 16 = 16-B aligned) and in place vs a separate
 output stream.  usage: python tools/ab_relay_layout.py [--n 1048576] [--pb 1472]
@@ -57,6 +58,7 @@ def main():
         dst = src if inplace else torch.zeros_like(src)
         off = torch.from_numpy(np.arange(n, dtype=np.uint64) * stride + hdr).to("cuda")
         ts = [[] for _ in ctxs]
+        td = [[] for _ in ctxs]
         ok = [True for _ in ctxs]
         for r in range(args.rounds + 1):
             for k, ck in enumerate(ctxs):
@@ -70,10 +72,19 @@ def main():
                 if r:
                     ts[k].append(e0.elapsed_time(e1))
                 ok[k] = ok[k] and torch.equal(dst[hdr: hdr + n * stride].view(n, stride)[:, :pb].reshape(-1), ref)
+                # decrypt the stream just encrypted: in place, or into the (plaintext) source stream
+                back = dst if inplace else src
+                e0.record(s)
+                ck.decrypt_ragged(dst, back, off, nb, n, stream=s.cuda_stream)
+                e1.record(s)
+                torch.cuda.synchronize()
+                if r:
+                    td[k].append(e0.elapsed_time(e1))
+                ok[k] = ok[k] and torch.equal(back[hdr: hdr + n * stride].view(n, stride)[:, :pb].reshape(-1), pt)
         for k, p in enumerate(libs):
-            print("%-22s %8d x %5d B stride %5d: enc %.4f ms (min %.4f)  %s  %s" %
-                  (label, n, pb, stride, statistics.median(ts[k]), min(ts[k]), "ok" if ok[k] else "MISMATCH",
-                   os.path.basename(p) if p else ""), flush=True)
+            print("%-22s %8d x %5d B stride %5d: enc %.4f ms (min %.4f) dec %.4f ms (min %.4f)  %s  %s" %
+                  (label, n, pb, stride, statistics.median(ts[k]), min(ts[k]), statistics.median(td[k]), min(td[k]),
+                   "ok" if ok[k] else "MISMATCH", os.path.basename(p) if p else ""), flush=True)
         del src, dst
         torch.cuda.empty_cache()
 
