@@ -298,14 +298,14 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     uint32_t dk_id = 0;  // KEYED: session whose schedule dk0 holds (~0u: none yet)
     if (KEYED) dk_id = ~0u;
     else if (!SESS) load_sched(a.keys, 0, 1, dk0);
-    // Work ranges [t * range_blocks, +range_blocks): taken from the launch's
-    // ticket counter (dyn), so a wave on a faster CU takes more of them and the
-    // waves finish within about one range of each other; or (static) wave w
+    // Work ranges [t * range_blocks, +range_blocks): each workgroup's share
+    // taken in order by its waves from its ticket counter (dyn), so the waves
+    // of a CU finish within about one range of each other; or (static) wave w
     // takes ranges w, w + nwaves, ...  KEYED (per-lane keys) and IV (IV
     // arrays): one static range per wave, as the runtime launches them (the
     // range loop around their larger step bodies cost VGPR spills).
     const uint32_t nwaves = gridDim.x * (kDecThreads / 64);
-    uint32_t ticket = a.dyn ? next_ticket(a.work) : (uint32_t)wave;
+    uint32_t ticket = a.dyn ? next_ticket(a.work, a.per_wg, (uint32_t)a.nranges) : (uint32_t)wave;
     while (true) {
         // The range's parameters are re-read from the kernel arguments here (an
         // opaque pointer keeps the loads in this block) instead of being held in
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
                                                       out_s);
         }
         if (KEYED || IV) break;
-        ticket = ka->dyn ? next_ticket(ka->work) : ticket + nwaves;
+        ticket = ka->dyn ? next_ticket(ka->work, ka->per_wg, (uint32_t)ka->nranges) : ticket + nwaves;
     }
 }
 

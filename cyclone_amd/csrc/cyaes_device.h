@@ -248,13 +248,21 @@ __device__ __forceinline__ uint32_t* dec_lead_word(uint32_t* work) { return work
 template <typename T>
 using KernArg = const __attribute__((address_space(4))) T*;
 
-// The wave's next work ticket (wave-uniform): one atomic on the launch's
-// ticket counter, from the first active lane.
-__device__ __forceinline__ uint32_t next_ticket(uint32_t* ctr) {
+// The wave's next work ticket (wave-uniform): one atomic on its workgroup's
+// ticket counter, from the first active lane.  Workgroup g owns tickets
+// [g * per, min((g + 1) * per, n)) and its waves take them in order, so the
+// 16 waves of a CU finish within about one range of each other; returns n
+// when the workgroup's share is done.  (One counter for the whole grid was
+// measured at ~88 M tickets/s, a ticket per 2-step range asks ~190 M/s: the
+// decrypt ran 2x slower.  A workgroup's own counter: ~430 ns per ticket,
+// uncontended; tools/atomicbench.hip, profiles/r04/atomicbench.jsonl.)
+__device__ __forceinline__ uint32_t next_ticket(uint32_t* work, uint32_t per, uint32_t n) {
     const uint32_t fl = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
     uint32_t t = 0;
-    if (__lane_id() == fl) t = atomicAdd(ctr, 1u);
-    return __builtin_amdgcn_readfirstlane(t);
+    if (__lane_id() == fl) t = atomicAdd(work + kWorkCtrOff + 64 * blockIdx.x, 1u);
+    t = __builtin_amdgcn_readfirstlane(t);
+    const uint32_t g0 = blockIdx.x * per;
+    return t < per && g0 < n ? min(g0 + t, n) : n;
 }
 
 // Decrypts N independent blocks together (N-way ILP per LDS round trip) and

@@ -97,12 +97,14 @@ struct EncArgs {
     uint32_t sess_payloads;  // uniform lane kernel: payloads_per_key when every wave lies in one session (SESS), else 0
 };
 
-// Per-launch decrypt scratch (DecArgs.work): word 0 is the range ticket
-// counter, words kWorkLeadOff + workgroup are the progress-feedback leader
-// words.  Per launch, so concurrent decrypts on different streams never share
-// them.
-constexpr uint32_t kWorkLeadOff = 64;  // its own 256-B line, away from the hot counter
-constexpr uint32_t dec_work_words(uint32_t grid) { return kWorkLeadOff + grid; }
+// Per-launch decrypt scratch (DecArgs.work): words kWorkLeadOff + workgroup
+// are the progress-feedback leader words, words kWorkCtrOff + 64 * workgroup
+// the workgroups' range ticket counters (a 256-B line each: a counter is only
+// touched by its own workgroup's waves).  Per launch, so concurrent decrypts
+// on different streams never share them.
+constexpr uint32_t kWorkLeadOff = 64;
+constexpr uint32_t kWorkCtrOff = 512;
+constexpr uint32_t dec_work_words(uint32_t grid) { return kWorkCtrOff + 64 * grid; }
 
 struct DecArgs {
     const uint8_t* in;
@@ -114,7 +116,9 @@ struct DecArgs {
     uint64_t range_blocks;    // flat kernel: blocks per work range (a multiple of 64*kDecRows)
     uint64_t nranges;         // flat kernel: ranges; ragged kernel: payload groups
     uint32_t* work;           // per-launch scratch (dec_work_words, zeroed before the launch): ticket counter, progress words
-    uint32_t dyn;             // 1: waves take ranges / groups from the ticket counter; 0: wave w takes w, w + nwaves, ...
+    uint32_t dyn;             // 1: workgroup g owns ranges / groups [g*per_wg, (g+1)*per_wg), its waves take them
+                              //    from its ticket counter; 0: wave w takes w, w + nwaves, ...
+    uint32_t per_wg;          // dyn: ranges / groups per workgroup
     Fastdiv bpp;              // flat kernel: blocks per payload
     uint32_t step_q, step_r;  // (64*kDecRows) / bpp, % bpp
     KeySel keys;

@@ -221,10 +221,10 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         load_sched(a.keys, 0, 1, dk0);
         dk_id = 0;
     }
-    // Groups from the launch's ticket counter (dyn: a wave on a faster CU takes
-    // more of them), or wave w takes w, w + nwaves, ...
-    for (uint64_t grp = a.dyn ? next_ticket(a.work) : wave0; grp < ngroups;
-         grp = a.dyn ? next_ticket(a.work) : grp + nwaves) {
+    // Groups from the workgroup's share in order, through its ticket counter
+    // (dyn: the waves of a CU finish together), or wave w takes w, w + nwaves, ...
+    for (uint64_t grp = a.dyn ? next_ticket(a.work, a.per_wg, (uint32_t)ngroups) : wave0; grp < ngroups;
+         grp = a.dyn ? next_ticket(a.work, a.per_wg, (uint32_t)ngroups) : grp + nwaves) {
         const uint64_t p0 = grp * G;
         const uint32_t gn = (uint32_t)min<uint64_t>(G, a.npayloads - p0);
         const bool holder = lane < gn;

@@ -284,6 +284,7 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     st = work.get(ctx->pool, 4ull * ww, stream);
     if (st) return st;
     a.work = static_cast<uint32_t*>(work.p);
+    a.per_wg = (uint32_t)((a.nranges + grid - 1) / grid);
     if (in == out && a.nranges > 1) {
         st = boundary.get(ctx->pool, a.nranges * sizeof(uint4), stream);
         if (st) return st;
@@ -335,6 +336,7 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     st = work.get(ctx->pool, 4ull * ww, stream);
     if (st) return st;
     a.work = static_cast<uint32_t*>(work.p);
+    a.per_wg = (uint32_t)((a.nranges + grid - 1) / grid);
     if (a.dyn) CY_TRY(launch_dec_prepass(a, ww, stream));
     return map_err(launch_decrypt_ragged(a, grid, sh.threads, stream));
 }

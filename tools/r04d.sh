@@ -11,8 +11,8 @@ L=cyclone_amd/libcyaes.so
 timeout -k 10 150 python tools/ab.py $L $L:CYAES_DEC_DYN=0 build/variants/decitl.so --payloads 1048576 --payload-bytes 1472 --rounds 8 > $O/ab_B.txt 2>&1
 timeout -k 10 150 python tools/ab.py $L $L:CYAES_DEC_DYN=0 build/variants/decitl.so --rounds 4 > $O/ab_C.txt 2>&1
 timeout -k 10 150 python tools/ab.py $L $L:CYAES_DEC_DYN=0 build/variants/decitl.so --payloads 1048576 --payload-bytes 1472 --ppk 256 --rounds 8 > $O/ab_D.txt 2>&1
-timeout -k 10 150 python tools/ab.py $L $L:CYAES_DEC_DYN=0 build/variants/decitl.so --payloads 1048576 --payload-bytes 1472 --relay --rounds 8 > $O/ab_relay_ragged.txt 2>&1
-timeout -k 10 150 python tools/ab.py $L $L:CYAES_DEC_DYN=0 build/variants/decitl.so --payloads 1048576 --payload-bytes 1472 --relay --relay-api strided --rounds 8 > $O/ab_relay_strided.txt 2>&1
+timeout -k 10 150 python tools/ab.py $L $L:CYAES_DEC_DYN=0 build/variants/decitl.so build/variants/allitl.so --payloads 1048576 --payload-bytes 1472 --relay --rounds 8 > $O/ab_relay_ragged.txt 2>&1
+timeout -k 10 150 python tools/ab.py $L $L:CYAES_DEC_DYN=0 build/variants/decitl.so build/variants/allitl.so --payloads 1048576 --payload-bytes 1472 --relay --relay-api strided --rounds 8 > $O/ab_relay_strided.txt 2>&1
 for cfg in B relay C D; do
   timeout -k 10 120 python tools/timeline.py --config $cfg --reps 2 > $O/timeline_$cfg.txt 2>&1
   timeout -k 10 120 python tools/timeline.py --config $cfg --reps 1 CYAES_DEC_DYN=0 > $O/timeline_${cfg}_static.txt 2>&1
