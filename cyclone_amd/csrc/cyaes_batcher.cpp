@@ -1002,32 +1002,38 @@ static int pin_span(cyaes_batcher* b, uintptr_t lo, uintptr_t hi, std::vector<si
         for (const PinEnt& p : added) (void)hipHostUnregister(reinterpret_cast<void*>(p.lo));
         (void)hipGetLastError();
     };
-    auto registered = [](uintptr_t q, uintptr_t* lo_out, uintptr_t* hi_out) {
+    // The registration holding page q, if one does: its base as
+    // hipMemGetAddressRange reports it (the registration's DEVICE range, not
+    // the host one: tools/hostreg_probe.hip, profiles/r04/hostreg_probe.txt),
+    // only compared between pages here.
+    auto registration = [](uintptr_t q, uintptr_t* base) {
         hipDeviceptr_t rb = nullptr;
         size_t rs = 0;
         if (hipMemGetAddressRange(&rb, &rs, reinterpret_cast<hipDeviceptr_t>(q)) != hipSuccess) {
             (void)hipGetLastError();
             return false;
         }
-        *lo_out = (uintptr_t)rb;
-        *hi_out = (uintptr_t)rb + rs;
+        *base = (uintptr_t)rb;
         return true;
     };
     for (const auto& g : gaps) {
         // Pages someone else registered (hipHostMalloc, the caller's own
-        // hipHostRegister): one such registration must hold the whole gap, and
-        // is then used as it is.  Never register over part of another owner's
-        // registration: HIP then accepts the overlapping range, but unregistering
-        // either one corrupts the other's record (measured: the other owner's
-        // hipHostUnregister fails afterwards).  Checked page by page.
-        uintptr_t rlo = 0, rhi = 0;
-        if (registered(g.first, &rlo, &rhi)) {
-            if (rlo <= g.first && g.second <= rhi) continue;
-            rollback();
-            return CYAES_EINVAL;
+        // hipHostRegister): one such registration must hold every page of the
+        // gap, and is then used as it is.  Never register over part of another
+        // owner's registration: HIP accepts the overlapping range, but
+        // unregistering either one corrupts the other's record (measured: the
+        // other owner's hipHostUnregister fails afterwards).  Checked page by page.
+        uintptr_t rb0 = 0, rb = 0;
+        if (registration(g.first, &rb0)) {
+            for (uintptr_t q = g.first + 4096; q < g.second; q += 4096)
+                if (!registration(q, &rb) || rb != rb0) {
+                    rollback();
+                    return CYAES_EINVAL;
+                }
+            continue;
         }
         for (uintptr_t q = g.first + 4096; q < g.second; q += 4096)
-            if (registered(q, &rlo, &rhi)) {
+            if (registration(q, &rb)) {
                 rollback();
                 return CYAES_EINVAL;
             }

@@ -19,9 +19,39 @@ static void q(const char* what, uint8_t* base, uint8_t* p) {
         printf("%-34s page %+.2f -> %s\n", what, (p - base) / 4096.0, hipGetErrorName(e));
 }
 
+// The addresses each query returns for host page q of a registration: the
+// host pointer, hipHostGetDevicePointer, hipMemGetAddressRange's base, and
+// hipPointerGetAttributes' device and host pointers (relative to q, in bytes).
+static void addrs(const char* what, uint8_t* q) {
+    void* dq = nullptr;
+    hipDeviceptr_t rb = nullptr;
+    size_t rs = 0;
+    hipPointerAttribute_t at = {};
+    const hipError_t e1 = hipHostGetDevicePointer(&dq, q, 0);
+    const hipError_t e2 = hipMemGetAddressRange(&rb, &rs, (hipDeviceptr_t)q);
+    const hipError_t e3 = hipPointerGetAttributes(&at, q);
+    (void)hipGetLastError();
+    printf("%-24s devptr %s %+lld | range %s base %+lld size %zu | attrs %s type %d dev %+lld host %+lld\n", what,
+           hipGetErrorName(e1), (long long)((uint8_t*)dq - q), hipGetErrorName(e2), (long long)((uint8_t*)rb - q), rs,
+           hipGetErrorName(e3), (int)at.type, (long long)((uint8_t*)at.devicePointer - q),
+           (long long)((uint8_t*)at.hostPointer - q));
+}
+
 int main() {
     uint8_t* m = (uint8_t*)aligned_alloc(4096, 16 * 4096);
     uint8_t* P = m;  // page 0
+    {  // flags 0 (what torch's cudaHostRegister passes) and mapped, queried at the start and inside
+        uint8_t* a = P + 8 * 4096;
+        printf("register [8,12) flags 0: %s\n", hipGetErrorName(hipHostRegister(a, 4 * 4096, 0)));
+        addrs("flags0 page 8", a);
+        addrs("flags0 page 9 + 100", a + 4096 + 100);
+        (void)hipHostUnregister(a);
+        printf("register [8,12) mapped: %s\n", hipGetErrorName(hipHostRegister(a, 4 * 4096, hipHostRegisterMapped)));
+        addrs("mapped page 8", a);
+        addrs("mapped page 9 + 100", a + 4096 + 100);
+        (void)hipHostUnregister(a);
+        (void)hipGetLastError();
+    }
     printf("register [1,5): %s\n", hipGetErrorName(hipHostRegister(P + 4096, 4 * 4096, hipHostRegisterMapped)));
     for (int i = 0; i <= 6; i++) q("after [1,5)", P, P + i * 4096 + (i == 2 ? 100 : 0));
     printf("register [5,7): %s\n", hipGetErrorName(hipHostRegister(P + 5 * 4096, 2 * 4096, hipHostRegisterMapped)));
