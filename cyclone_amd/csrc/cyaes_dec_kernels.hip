@@ -7,6 +7,10 @@
 #define CYAES_TU 2
 #include "cyaes_device.h"
 
+#ifndef CYAES_DEC_TICKET_AHEAD
+#define CYAES_DEC_TICKET_AHEAD 0
+#endif
+
 namespace cyaes {
 namespace {
 
@@ -306,6 +310,9 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     // range loop around their larger step bodies cost VGPR spills).
     const uint32_t nwaves = gridDim.x * (kDecThreads / 64);
     uint32_t ticket = a.dyn ? next_ticket(a.work, a.per_wg, (uint32_t)a.nranges) : (uint32_t)wave;
+#if CYAES_DEC_TICKET_AHEAD
+    uint32_t ahead = 0;  // dyn: the next range's ticket, issued at this range's start
+#endif
     while (true) {
         // The range's parameters are re-read from the kernel arguments here (an
         // opaque pointer keeps the loads in this block) instead of being held in
@@ -315,6 +322,9 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
         KernArg<DecArgs> ka = (KernArg<DecArgs>)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(ka));
         if (ticket >= ka->nranges) break;
+#if CYAES_DEC_TICKET_AHEAD
+        if (ka->dyn) ahead = ticket_issue(ka->work);
+#endif
         const uint64_t begin = (uint64_t)ticket * ka->range_blocks;
         const uint64_t end = min(begin + ka->range_blocks, ka->nblocks);
         FlatPos ps;
@@ -387,7 +397,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
                                                       out_s);
         }
         if (KEYED || IV) break;
+#if CYAES_DEC_TICKET_AHEAD
+        ticket = ka->dyn ? ticket_resolve(ahead, ka->per_wg, (uint32_t)ka->nranges) : ticket + nwaves;
+#else
         ticket = ka->dyn ? next_ticket(ka->work, ka->per_wg, (uint32_t)ka->nranges) : ticket + nwaves;
+#endif
     }
 }
 

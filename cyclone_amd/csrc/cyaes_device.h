@@ -256,6 +256,19 @@ using KernArg = const __attribute__((address_space(4))) T*;
 // measured at ~88 M tickets/s, a ticket per 2-step range asks ~190 M/s: the
 // decrypt ran 2x slower.  A workgroup's own counter: ~430 ns per ticket,
 // uncontended; tools/atomicbench.hip, profiles/r04/atomicbench.jsonl.)
+// Split form (CYAES_DEC_TICKET_AHEAD): issue the atomic now, resolve the
+// ticket later, so its round trip overlaps a range's work.
+__device__ __forceinline__ uint32_t ticket_issue(uint32_t* work) {
+    const uint32_t fl = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
+    uint32_t t = 0;
+    if (__lane_id() == fl) t = atomicAdd(work + kWorkCtrOff + 64 * blockIdx.x, 1u);
+    return t;  // valid in lane fl only
+}
+__device__ __forceinline__ uint32_t ticket_resolve(uint32_t t, uint32_t per, uint32_t n) {
+    t = __builtin_amdgcn_readfirstlane(t);
+    const uint32_t g0 = blockIdx.x * per;
+    return t < per && g0 < n ? min(g0 + t, n) : n;
+}
 __device__ __forceinline__ uint32_t next_ticket(uint32_t* work, uint32_t per, uint32_t n) {
     const uint32_t fl = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
     uint32_t t = 0;

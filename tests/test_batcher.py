@@ -861,3 +861,33 @@ def test_device_relay_stream_strided(chunk, mode):
     with pytest.raises(ca.CyaesError):  # stride shorter than the payload
         ctx.decrypt_strided(dev, dev, first, pb - 16, n, pb)
     ctx.close()
+
+
+def test_strided_batch_session_keys():
+    """Strided batches with per-session keys (payloads_per_key and a key index
+    array) run as ragged batches with lists written on the device; the bytes
+    between payloads are untouched and every payload matches the oracle under
+    its own key (relay_server.cpp:218-240 gives each connection its key)."""
+    import numpy as np
+    import torch
+    rng = np.random.default_rng(61)
+    n, pb, stride, first, ppk = 300, 1472, 1500, 20, 7
+    nk = (n + ppk - 1) // ppk
+    keys = [oracle.session_key(s) for s in range(nk)]
+    ctx = ca.GpuContext(0)
+    ctx.set_keys(b"".join(keys))
+    buf = rng.integers(0, 256, first + n * stride + 64, dtype=np.uint8)
+    pt = np.stack([buf[first + p * stride: first + p * stride + pb] for p in range(n)]).reshape(-1)
+    want = oracle.batch(False, keys, ppk, pt, pb, nthreads=8)
+    d = torch.from_numpy(buf.copy()).cuda()
+    ctx.encrypt_strided(d, d, first, stride, n, pb, payloads_per_key=ppk)
+    got = d.cpu().numpy()
+    for p in range(n):
+        o = first + p * stride
+        assert np.array_equal(got[o:o + pb], want[p * pb:(p + 1) * pb]), p
+        assert np.array_equal(got[o + pb:o + stride], buf[o + pb:o + stride])
+    kidx = torch.from_numpy((np.arange(n) // ppk).astype(np.uint32)).cuda()
+    ctx.decrypt_strided(d, d, first, stride, n, pb, key_idx=kidx)
+    assert np.array_equal(d.cpu().numpy(), buf)
+    assert ctx.check() == ca.CYAES_OK
+    ctx.close()
