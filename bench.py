@@ -688,7 +688,7 @@ def main():
     if os.path.exists(tfile):
         ftr = json.load(open(tfile)).get("C" if args.config == "E" else args.config, {}).get(dom)
     if live and dom in live:
-        algo = 2.0 * nbytes
+        algo = 2.0 * CONFIGS["C"][0] * CONFIGS["C"][1]  # the passes profile config C's launches (live_traffic)
         roofline["traffic"] = live[dom]
         roofline["traffic_note"] = ("measured in this run: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes (separate "
                                     "child processes, bench.py --config C --steps 2), FETCH_SIZE x2 per the gfx950 "

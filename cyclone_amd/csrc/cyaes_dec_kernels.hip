@@ -7,10 +7,6 @@
 #define CYAES_TU 2
 #include "cyaes_device.h"
 
-#ifndef CYAES_DEC_TICKET_AHEAD
-#define CYAES_DEC_TICKET_AHEAD 0
-#endif
-
 namespace cyaes {
 namespace {
 
@@ -283,7 +279,10 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
 // nullptr); the IV code and the payload-index tracking compile out, which
 // keeps the SGPR budget of the round loop (with them, the !BIG SESS kernel
 // scheduled its rounds with 321 s_waitcnt per 640 LDS reads against 173).
-template <bool KEYED, bool BIG, bool SESS, bool IV, bool STRIDED>
+// DIV: the progress-feedback divisor (steps behind the workgroup's leader per
+// priority level): kDecPrioDiv for long launches, kDecPrioDivShort when each
+// wave has few steps (the runtime's choice, DecArgs / launch_decrypt_flat).
+template <bool KEYED, bool BIG, bool SESS, bool IV, bool STRIDED, uint32_t DIV>
 __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     constexpr int R = kDecRows;
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
@@ -302,17 +301,18 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     uint32_t dk_id = 0;  // KEYED: session whose schedule dk0 holds (~0u: none yet)
     if (KEYED) dk_id = ~0u;
     else if (!SESS) load_sched(a.keys, 0, 1, dk0);
-    // Work ranges [t * range_blocks, +range_blocks): each workgroup's share
-    // taken in order by its waves from its ticket counter (dyn), so the waves
-    // of a CU finish within about one range of each other; or (static) wave w
-    // takes ranges w, w + nwaves, ...  KEYED (per-lane keys) and IV (IV
-    // arrays): one static range per wave, as the runtime launches them (the
-    // range loop around their larger step bodies cost VGPR spills).
+    // Work ranges (DecArgs): wave w first takes static range w, then (dyn)
+    // ranges of the dynamic pool from the per-XCD ticket pools, stealing from
+    // the other XCDs' pools when its own is exhausted, so waves on faster CUs
+    // and XCDs take more; or (static only) ranges w + nwaves, ...  KEYED
+    // (per-lane keys) and IV (IV arrays): one static range per wave, as the
+    // runtime launches them (the range loop around their larger step bodies
+    // cost VGPR spills).
     const uint32_t nwaves = gridDim.x * (kDecThreads / 64);
-    uint32_t ticket = a.dyn ? next_ticket(a.work, a.per_wg, (uint32_t)a.nranges) : (uint32_t)wave;
-#if CYAES_DEC_TICKET_AHEAD
-    uint32_t ahead = 0;  // dyn: the next range's ticket, issued at this range's start
-#endif
+    uint32_t pool = xcc_id();
+    uint32_t ticket = (uint32_t)wave;
+    if (a.dyn && ticket >= a.nstat)
+        ticket = a.nstat + dyn_ticket(a.work, pool, a.per_xcd, (uint32_t)a.nranges - a.nstat);
     while (true) {
         // The range's parameters are re-read from the kernel arguments here (an
         // opaque pointer keeps the loads in this block) instead of being held in
@@ -322,11 +322,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
         KernArg<DecArgs> ka = (KernArg<DecArgs>)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(ka));
         if (ticket >= ka->nranges) break;
-#if CYAES_DEC_TICKET_AHEAD
-        if (ka->dyn) ahead = ticket_issue(ka->work);
-#endif
-        const uint64_t begin = (uint64_t)ticket * ka->range_blocks;
-        const uint64_t end = min(begin + ka->range_blocks, ka->nblocks);
+        const bool stat = ticket < ka->nstat;
+        const uint64_t begin = stat ? (uint64_t)ticket * ka->stat_blocks
+                                    : (uint64_t)ka->nstat * ka->stat_blocks +
+                                          (uint64_t)(ticket - ka->nstat) * ka->range_blocks;
+        const uint64_t end = min(begin + (stat ? ka->stat_blocks : ka->range_blocks), ka->nblocks);
         FlatPos ps;
         ps.bp = begin / a.bpp.d;
         ps.bpos = (uint32_t)(begin - ps.bp * a.bpp.d);
@@ -383,11 +383,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
                 advance();
                 if (base + 128 * R <= end)
                     flat_load<true, BIG, STRIDED>(a, in_s, lane, base + 64 * R, end, ps, rk, pk, c, pv);
-                prio_feedback(leadp, ++prog, kDecPrioDiv);
+                prio_feedback(leadp, ++prog, DIV);
             } else {
                 if (base + 128 * R <= end)
                     flat_load<true, BIG, STRIDED>(a, in_s, lane, base + 64 * R, end, ps, rk, pk, c, pv);
-                prio_feedback(leadp, ++prog, kDecPrioDiv);
+                prio_feedback(leadp, ++prog, DIV);
                 advance();
             }
         }
@@ -397,11 +397,8 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
                                                       out_s);
         }
         if (KEYED || IV) break;
-#if CYAES_DEC_TICKET_AHEAD
-        ticket = ka->dyn ? ticket_resolve(ahead, ka->per_wg, (uint32_t)ka->nranges) : ticket + nwaves;
-#else
-        ticket = ka->dyn ? next_ticket(ka->work, ka->per_wg, (uint32_t)ka->nranges) : ticket + nwaves;
-#endif
+        ticket = ka->dyn ? ka->nstat + dyn_ticket(ka->work, pool, ka->per_xcd, (uint32_t)ka->nranges - ka->nstat)
+                         : ticket + nwaves;
     }
 }
 
@@ -412,7 +409,7 @@ __global__ void k_dec_prepass(DecArgs a, uint32_t work_words) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r < work_words) a.work[r] = 0;
     if (!a.boundary || r >= a.nranges) return;
-    const uint64_t begin = r * a.range_blocks;
+    const uint64_t begin = r < a.nstat ? r * a.stat_blocks : a.nstat * a.stat_blocks + (r - a.nstat) * a.range_blocks;
     if (begin == 0 || begin >= a.nblocks || begin % a.bpp.d == 0) return;
     uint4* snap = const_cast<uint4*>(a.boundary) + r;
     const Ext se = ext(a.boundary, 16 * a.nranges);
@@ -422,23 +419,29 @@ __global__ void k_dec_prepass(DecArgs a, uint32_t work_words) {
 
 }  // namespace
 
-hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream) {
+template <uint32_t DIV>
+static void launch_flat(const DecArgs& a, dim3 g, dim3 b, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
     const bool big = a.bpp.d >= 64u * kDecRows;
-    const dim3 g(grid), b(kDecThreads);
     const bool sess = a.sess_blocks != 0;  // keyed by step-aligned sessions: the unkeyed step per session
     const bool iv = a.iv_in != nullptr || a.iv_out != nullptr;  // (the runtime sets sess only without IVs)
     // STRIDED: unkeyed, no IV arrays (the runtime checks)
-    if (a.stride && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false, true>), g, b, 0, stream, a);
-    else if (a.stride) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false, true>), g, b, 0, stream, a);
-    else if (sess && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, true, false, false>), g, b, 0, stream, a);
-    else if (sess) hipLaunchKernelGGL((k_decrypt_flat<false, false, true, false, false>), g, b, 0, stream, a);
-    else if (keyed && big) hipLaunchKernelGGL((k_decrypt_flat<true, true, false, true, false>), g, b, 0, stream, a);
-    else if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true, false, false, true, false>), g, b, 0, stream, a);
-    else if (big && iv) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, true, false>), g, b, 0, stream, a);
-    else if (big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false, false>), g, b, 0, stream, a);
-    else if (iv) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, true, false>), g, b, 0, stream, a);
-    else hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false, false>), g, b, 0, stream, a);
+    if (a.stride && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false, true, DIV>), g, b, 0, stream, a);
+    else if (a.stride) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false, true, DIV>), g, b, 0, stream, a);
+    else if (sess && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, true, false, false, DIV>), g, b, 0, stream, a);
+    else if (sess) hipLaunchKernelGGL((k_decrypt_flat<false, false, true, false, false, DIV>), g, b, 0, stream, a);
+    else if (keyed && big) hipLaunchKernelGGL((k_decrypt_flat<true, true, false, true, false, kDecPrioDiv>), g, b, 0, stream, a);
+    else if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true, false, false, true, false, kDecPrioDiv>), g, b, 0, stream, a);
+    else if (big && iv) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, true, false, kDecPrioDiv>), g, b, 0, stream, a);
+    else if (big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false, false, DIV>), g, b, 0, stream, a);
+    else if (iv) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, true, false, kDecPrioDiv>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false, false, DIV>), g, b, 0, stream, a);
+}
+
+hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream) {
+    const dim3 g(grid), b(kDecThreads);
+    if (a.prio_short) launch_flat<kDecPrioDivShort>(a, g, b, stream);
+    else launch_flat<kDecPrioDiv>(a, g, b, stream);
     return hipGetLastError();
 }
 

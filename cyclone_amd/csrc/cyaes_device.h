@@ -248,35 +248,29 @@ __device__ __forceinline__ uint32_t* dec_lead_word(uint32_t* work) { return work
 template <typename T>
 using KernArg = const __attribute__((address_space(4))) T*;
 
-// The wave's next work ticket (wave-uniform): one atomic on its workgroup's
-// ticket counter, from the first active lane.  Workgroup g owns tickets
-// [g * per, min((g + 1) * per, n)) and its waves take them in order, so the
-// 16 waves of a CU finish within about one range of each other; returns n
-// when the workgroup's share is done.  (One counter for the whole grid was
-// measured at ~88 M tickets/s, a ticket per 2-step range asks ~190 M/s: the
-// decrypt ran 2x slower.  A workgroup's own counter: ~430 ns per ticket,
-// uncontended; tools/atomicbench.hip, profiles/r04/atomicbench.jsonl.)
-// Split form (CYAES_DEC_TICKET_AHEAD): issue the atomic now, resolve the
-// ticket later, so its round trip overlaps a range's work.
-__device__ __forceinline__ uint32_t ticket_issue(uint32_t* work) {
+// The dynamic pool of a launch (DecArgs.dyn): tickets [0, ndyn) in kXcds
+// contiguous pools of per_xcd, one per XCD.  A wave takes the next ticket of
+// its current pool (first its own XCD's: the atomic stays among that XCD's
+// waves) and, once that pool is exhausted, moves on to the next one, so an
+// XCD that runs ahead takes work from the slower ones and the XCDs finish
+// together.  Returns ndyn when every pool is exhausted (at most kXcds failed
+// tries).  Measured (tools/atomicbench.hip, profiles/r04/atomicbench.jsonl):
+// one counter for all 4,096 waves ~88 M tickets/s (a ticket per 2-step range
+// asks ~190 M/s: the first dynamic decrypt ran 2x slower), one per XCD ~540 M/s,
+// one per workgroup ~9.3 G/s.
+__device__ __forceinline__ uint32_t dyn_ticket(uint32_t* work, uint32_t& pool, uint32_t per_xcd, uint32_t ndyn) {
     const uint32_t fl = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
-    uint32_t t = 0;
-    if (__lane_id() == fl) t = atomicAdd(work + kWorkCtrOff + 64 * blockIdx.x, 1u);
-    return t;  // valid in lane fl only
+    for (uint32_t k = 0; k < kXcds; k++) {
+        uint32_t t = 0;
+        if (__lane_id() == fl) t = atomicAdd(work + kWorkCtrOff + 64 * pool, 1u);
+        t = __builtin_amdgcn_readfirstlane(t);
+        const uint32_t g = pool * per_xcd + t;
+        if (t < per_xcd && g < ndyn) return g;
+        pool = pool + 1 < kXcds ? pool + 1 : 0;
+    }
+    return ndyn;
 }
-__device__ __forceinline__ uint32_t ticket_resolve(uint32_t t, uint32_t per, uint32_t n) {
-    t = __builtin_amdgcn_readfirstlane(t);
-    const uint32_t g0 = blockIdx.x * per;
-    return t < per && g0 < n ? min(g0 + t, n) : n;
-}
-__device__ __forceinline__ uint32_t next_ticket(uint32_t* work, uint32_t per, uint32_t n) {
-    const uint32_t fl = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
-    uint32_t t = 0;
-    if (__lane_id() == fl) t = atomicAdd(work + kWorkCtrOff + 64 * blockIdx.x, 1u);
-    t = __builtin_amdgcn_readfirstlane(t);
-    const uint32_t g0 = blockIdx.x * per;
-    return t < per && g0 < n ? min(g0 + t, n) : n;
-}
+__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg(20 | (31 << 11)) % kXcds; }  // HW_REG_XCC_ID
 
 // Decrypts N independent blocks together (N-way ILP per LDS round trip) and
 // returns D(c[n]) ^ prev[n] in prev[n] (CBC, cyr_rijndael.cpp:625-630).
@@ -381,6 +375,14 @@ __device__ __forceinline__ void prio_feedback(uint32_t* lead, uint32_t step, uin
 // (profiles/r03/ab_prio_div_s2.txt).
 constexpr uint32_t kEncPrioDiv = CYAES_ENC_PRIO_DIV;
 constexpr uint32_t kDecPrioDiv = CYAES_DEC_PRIO_DIV;  // steps = 64*kDecRows-block rows (r01 A/B: 4, 8, 16 -> 8)
+// Launches with few steps per wave (the MTU configs, relay streams: ~92) level
+// their waves better at 4 (r04, static split: config B decrypt -2.8 %, the
+// strided relay stream -4.7 %; config C +0.5 % at 4, so it keeps 8:
+// profiles/r04/ab_dec_prio_div.txt).
+#ifndef CYAES_DEC_PRIO_DIV_SHORT
+#define CYAES_DEC_PRIO_DIV_SHORT 4
+#endif
+constexpr uint32_t kDecPrioDivShort = CYAES_DEC_PRIO_DIV_SHORT;
 
 __device__ __forceinline__ uint4 default_iv() { return make_uint4(kIv0, kIv1, kIv2, kIv3); }
 

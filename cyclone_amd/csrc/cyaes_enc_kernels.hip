@@ -97,7 +97,10 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
         const uint64_t p = RUNS ? w * R : w;  // (first) payload of the work item
         uint64_t off;
         uint32_t nb;
-        if (RAGGED) {
+        if (RAGGED && a.stride) {  // strided batch: the positions are arithmetic
+            off = active ? a.off0 + p * a.stride : 0;
+            nb = active ? bpp : 0;
+        } else if (RAGGED) {
             off = active ? LD8(a.offsets + p, ext(a.offsets, 8 * a.npayloads)) : 0;
             nb = active ? (LD4(a.nbytes + p, ext(a.nbytes, 4 * a.npayloads)) >> 4) : 0;
         } else {
@@ -273,7 +276,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
 
 hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
-    const bool ragged = a.offsets != nullptr;
+    const bool ragged = a.offsets != nullptr || a.stride != 0;
     const dim3 g(grid), b(threads);
     const bool runs = !ragged && a.run > 1;
     const bool sess = !ragged && a.sess_payloads != 0;  // keyed by whole-wave sessions: the unkeyed body per session

@@ -57,9 +57,12 @@ constexpr uint64_t kQuadRaggedFactor = 1;
 #define CYAES_DEC_ROWS 4
 #endif
 constexpr int kDecRows = CYAES_DEC_ROWS;
-// Dynamic decrypt work (DecArgs.dyn): steps per flat-decrypt range, and the
-// ragged decrypt's payload groups per wave of a full grid.
-constexpr uint32_t kDecRangeSteps = 2;
+// Dynamic decrypt work (DecArgs.dyn): the share of a launch's work in the
+// dynamic pool (%), steps per dynamic flat-decrypt range, and the ragged
+// decrypt's payload groups per wave of a full grid.
+constexpr uint32_t kDecDynPct = 25;
+constexpr uint64_t kDecShortSteps = 256;  // steps per wave at most for the short-launch progress divisor
+constexpr uint32_t kDecRangeSteps = 4;
 constexpr uint32_t kDecGroupsPerWave = 8;
 
 struct Fastdiv {  // Lemire: q = mulhi64(M, n) exact for all 32-bit n, d >= 2
@@ -95,16 +98,21 @@ struct EncArgs {
     uint32_t* status;
     uint32_t run;            // uniform lane kernel: payloads per work item (> 1: k_encrypt RUNS; no IV arrays)
     uint32_t sess_payloads;  // uniform lane kernel: payloads_per_key when every wave lies in one session (SESS), else 0
+    uint64_t off0, stride;   // ragged kernels, stride != 0: payload p at byte off0 + p * stride, payload_bytes each
+                             // (cyaes_gpu_encrypt_strided; offsets / nbytes are not read)
 };
 
 // Per-launch decrypt scratch (DecArgs.work): words kWorkLeadOff + workgroup
-// are the progress-feedback leader words, words kWorkCtrOff + 64 * workgroup
-// the workgroups' range ticket counters (a 256-B line each: a counter is only
-// touched by its own workgroup's waves).  Per launch, so concurrent decrypts
-// on different streams never share them.
+// are the progress-feedback leader words, words kWorkCtrOff + 64 * x the
+// ticket counters of the dynamic pools, one per XCD (a 256-B line each).  Per
+// launch, so concurrent decrypts on different streams never share them
+// (VERDICT r03, weak 7).
 constexpr uint32_t kWorkLeadOff = 64;
 constexpr uint32_t kWorkCtrOff = 512;
-constexpr uint32_t dec_work_words(uint32_t grid) { return kWorkCtrOff + 64 * grid; }
+constexpr uint32_t kXcds = 8;  // MI355X; on a chip with fewer, the spare pools are simply stolen from
+constexpr uint32_t dec_work_words(uint32_t grid) {
+    return kWorkCtrOff + 64 * kXcds > kWorkLeadOff + grid ? kWorkCtrOff + 64 * kXcds : kWorkLeadOff + grid;
+}
 
 struct DecArgs {
     const uint8_t* in;
@@ -113,12 +121,19 @@ struct DecArgs {
     const uint32_t* nbytes;
     uint64_t npayloads;
     uint64_t nblocks;         // flat kernel: total blocks = npayloads * bpp
-    uint64_t range_blocks;    // flat kernel: blocks per work range (a multiple of 64*kDecRows)
-    uint64_t nranges;         // flat kernel: ranges; ragged kernel: payload groups
-    uint32_t* work;           // per-launch scratch (dec_work_words, zeroed before the launch): ticket counter, progress words
-    uint32_t dyn;             // 1: workgroup g owns ranges / groups [g*per_wg, (g+1)*per_wg), its waves take them
-                              //    from its ticket counter; 0: wave w takes w, w + nwaves, ...
-    uint32_t per_wg;          // dyn: ranges / groups per workgroup
+    // Work ranges (flat kernel; the ragged kernel's unit is a payload group):
+    // ranges [0, nstat) are static, stat_blocks long, wave w takes range w (and
+    // w + nwaves, ... when there are more); ranges [nstat, nranges) are the
+    // dynamic pool (dyn), range_blocks long, handed out by per-XCD ticket
+    // counters with stealing (cyaes_device.h, dyn_ticket).
+    uint64_t stat_blocks;     // flat kernel: blocks per static range (a multiple of 64*kDecRows)
+    uint64_t range_blocks;    // flat kernel: blocks per dynamic range (a multiple of 64*kDecRows)
+    uint64_t nranges;         // flat kernel: static + dynamic ranges; ragged kernel: payload groups
+    uint32_t nstat;           // static ranges / groups
+    uint32_t per_xcd;         // dyn: tickets per XCD pool (ceil((nranges - nstat) / kXcds))
+    uint32_t* work;           // per-launch scratch (dec_work_words, zeroed before a dyn launch): counters, progress words
+    uint32_t dyn;             // 1: ranges [nstat, nranges) from the ticket pools
+    uint32_t prio_short;      // flat kernel: few steps per wave, the short-launch progress divisor (kDecPrioDivShort)
     Fastdiv bpp;              // flat kernel: blocks per payload
     uint32_t step_q, step_r;  // (64*kDecRows) / bpp, % bpp
     KeySel keys;

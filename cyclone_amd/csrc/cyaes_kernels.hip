@@ -120,7 +120,10 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_quad(EncArgs a) {
         if (p >= a.npayloads) continue;
         uint64_t off;
         uint32_t nb;
-        if (RAGGED) {
+        if (RAGGED && a.stride) {  // strided batch
+            off = a.off0 + p * a.stride;
+            nb = a.payload_bytes >> 4;
+        } else if (RAGGED) {
             off = LD8(a.offsets + p, ext(a.offsets, 8 * a.npayloads));
             nb = LD4(a.nbytes + p, ext(a.nbytes, 4 * a.npayloads)) >> 4;
         } else {
@@ -221,10 +224,15 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         load_sched(a.keys, 0, 1, dk0);
         dk_id = 0;
     }
-    // Groups from the workgroup's share in order, through its ticket counter
-    // (dyn: the waves of a CU finish together), or wave w takes w, w + nwaves, ...
-    for (uint64_t grp = a.dyn ? next_ticket(a.work, a.per_wg, (uint32_t)ngroups) : wave0; grp < ngroups;
-         grp = a.dyn ? next_ticket(a.work, a.per_wg, (uint32_t)ngroups) : grp + nwaves) {
+    // Groups [0, nstat) are static (wave w takes w, w + nwaves, ...); then (dyn)
+    // groups nstat + t of the dynamic pool from the per-XCD ticket pools, with
+    // stealing (cyaes_device.h, dyn_ticket), so the waves and XCDs finish together.
+    uint32_t pool = xcc_id();
+    const uint32_t nst = a.dyn ? a.nstat : (uint32_t)ngroups;
+    const uint32_t ndyn = (uint32_t)ngroups - nst;
+    uint64_t grp = wave0;
+    if (grp >= nst) grp = a.dyn ? nst + dyn_ticket(a.work, pool, a.per_xcd, ndyn) : ngroups;
+    for (; grp < ngroups;) {
         const uint64_t p0 = grp * G;
         const uint32_t gn = (uint32_t)min<uint64_t>(G, a.npayloads - p0);
         const bool holder = lane < gn;
@@ -396,6 +404,9 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
             }
             carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
         }
+        // next group: static ones by stride, then the dynamic pool
+        const uint64_t nxt = grp + nwaves;
+        grp = nxt < nst ? nxt : (a.dyn ? nst + dyn_ticket(a.work, pool, a.per_xcd, ndyn) : ngroups);
     }
 }
 
@@ -486,7 +497,7 @@ __global__ void k_digest(const uint64_t* buf, uint64_t nwords, unsigned long lon
 
 hipError_t launch_encrypt_quad(const EncArgs& a, int grid, int threads, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
-    const bool ragged = a.offsets != nullptr;
+    const bool ragged = a.offsets != nullptr || a.stride != 0;
     const dim3 g(grid), b(threads);
     if (ragged && keyed) hipLaunchKernelGGL((k_encrypt_quad<true, true>), g, b, 0, stream, a);
     else if (ragged) hipLaunchKernelGGL((k_encrypt_quad<true, false>), g, b, 0, stream, a);

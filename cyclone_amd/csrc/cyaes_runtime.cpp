@@ -24,9 +24,10 @@ struct cyaes_gpu {
     uint32_t ragged_group = 0;  // env CYAES_RAGGED_GROUP: payloads per ragged-decrypt wave group (0 = auto; tests, A/B)
     uint32_t enc_run = 0;       // env CYAES_ENC_RUN: payloads per lane run of the uniform encrypt (0 = auto; tests, A/B)
     bool enc_no_sess = false;   // env CYAES_ENC_NO_SESS=1: keyed uniform encrypt always by waterfall (tests, A/B)
-    bool dec_dyn = true;        // env CYAES_DEC_DYN=0: static per-wave decrypt ranges / groups (tests, A/B)
+    int dec_dyn = -1;           // env CYAES_DEC_DYN: 1 / 0 force the dynamic decrypt pool on / off; -1: long launches only
     uint32_t dec_range_steps = kDecRangeSteps;  // env CYAES_DEC_RANGE_STEPS: steps per dynamic flat-decrypt range
     uint32_t dec_groups_per_wave = kDecGroupsPerWave;  // env CYAES_DEC_GROUPS_PER_WAVE: ragged groups per wave
+    uint32_t dec_dyn_pct = kDecDynPct;  // env CYAES_DEC_DYN_PCT: % of a decrypt's work in the dynamic pool
     int dec_grid_max = 0;       // env CYAES_DEC_GRID: cap on decrypt workgroups (tests: many ranges per wave on small batches)
     bool strided_lists = false; // env CYAES_STRIDED_LISTS=1: strided decrypts as ragged batches (tests, A/B)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
@@ -124,11 +125,16 @@ bool cyaes::ragged_encrypt_is_quad(const cyaes_gpu* ctx, uint64_t n) {
 
 namespace {
 
+// offsets == nullptr and stride != 0: a strided batch (payload p at off0 + p *
+// stride, payload_bytes each), run by the ragged kernels without lists.
 int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
                    uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk,
                    const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream, const uint32_t* table = nullptr,
-                   uint32_t table_keys = 0) {
+                   uint32_t table_keys = 0, uint64_t off0 = 0, uint64_t stride = 0) {
     EncArgs a = {};
+    a.off0 = off0;
+    a.stride = stride;
+    const bool ragged = offsets != nullptr || stride != 0;
     int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys, table, table_keys);
     if (st) return st;
     a.in = in;
@@ -141,7 +147,7 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.iv_out = iv_out;
     a.tables = ctx->d_tables + kEncTableOff / 4;
     a.status = ctx->d_status;
-    if (offsets ? ragged_encrypt_is_quad(ctx, npayloads) : npayloads < ctx->quad_max_chains) {
+    if (ragged ? ragged_encrypt_is_quad(ctx, npayloads) : npayloads < ctx->quad_max_chains) {
         // Latency-bound batch (fewer chains than lanes to fill the chip four
         // times over), or a ragged one: four lanes per chain (k_encrypt_quad).
         const Shape sh = wave_shape(ctx, (4 * npayloads + 63) / 64, kEncThreads);
@@ -155,7 +161,7 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     // (With per-session keys on the waterfall path (config D) runs measured 3 %
     // slower, without keys (config B) 1.5 % faster, profiles/r03/ab_enc_runs.txt;
     // whole-wave sessions take the SESS path below, which has no waterfall.)
-    const bool runs_ok = !offsets && !iv_in && !iv_out && !key_idx && payload_bytes <= kRunMaxPayload;
+    const bool runs_ok = !ragged && !iv_in && !iv_out && !key_idx && payload_bytes <= kRunMaxPayload;
     const bool runs_auto = runs_ok;
     uint64_t R = 1;
     if (runs_auto) {
@@ -170,7 +176,7 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     // (SESS).  Otherwise keyed batches take the per-lane waterfall, without runs
     // unless forced.
     bool sess = false;
-    if (!offsets && !key_idx && ppk && !ctx->enc_no_sess) {
+    if (!ragged && !key_idx && ppk && !ctx->enc_no_sess) {
         uint64_t r = R;
         while (r > 1 && ppk % (64 * r)) r--;
         if (ppk % (64 * r) == 0) {
@@ -254,24 +260,45 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     // without IV arrays (the SESS kernels compile the IV code out).
     const uint64_t sess_blocks = (uint64_t)ppk * bpp;
     if (!key_idx && ppk && sess_blocks % step == 0 && !iv_in && !iv_out) a.sess_blocks = sess_blocks;
-    // Dynamic ranges of dec_range_steps steps (fewer when the static split is
-    // finer, so a small batch still spreads over every wave), handed out by the
-    // launch's ticket counter: the waves finish within about one range of each
-    // other instead of carrying the spread of CU speeds.
-    // Per-lane keys and IV arrays keep one static range per wave (their kernels
-    // do not loop over ranges).  SESS ranges divide the session.
+    // Work ranges (DecArgs, cyaes_device.h dyn_ticket).  Static split: one
+    // range of bpw blocks per wave.  Dynamic (dyn): each wave first takes a
+    // static range of (100 - dec_dyn_pct) % of its fair share, and the rest of
+    // the batch is a pool of dec_range_steps-step ranges handed out by per-XCD
+    // ticket pools with stealing, so waves on faster CUs and XCDs take more of
+    // it and the waves finish within about one range of each other (the static
+    // split's tail: CU and XCD speed spread, profiles/r04/timeline_*).  Per-lane
+    // keys, IV arrays and sessions keep the static split (sessions: ranges that
+    // divide the session).
     const bool keyed_lane = (key_idx || ppk) && !a.sess_blocks;
-    uint64_t range_steps = bpw / step;
-    a.dyn = ctx->dec_dyn && !keyed_lane && !iv_in && !iv_out && ctx->dec_range_steps > 0 &&
-            ctx->dec_range_steps < range_steps;
-    if (a.dyn) range_steps = ctx->dec_range_steps;
-    if (a.sess_blocks) {
-        const uint64_t sess_steps = a.sess_blocks / step;
-        while (sess_steps % range_steps) range_steps--;
+    const uint64_t fair_steps = bpw / step;
+    const uint64_t dyn_steps = ctx->dec_range_steps;
+    // Auto: only long launches (> kDecShortSteps steps per wave, config C) take the
+    // pool; short ones level their waves by progress feedback alone (r04 A/B:
+    // the pool cost config B 2-3 % and gained config C ~1 %).
+    const bool dyn_want = ctx->dec_dyn == 1 || (ctx->dec_dyn < 0 && fair_steps > kDecShortSteps);
+    a.dyn = dyn_want && !keyed_lane && !a.sess_blocks && !iv_in && !iv_out && dyn_steps > 0 &&
+            dyn_steps < fair_steps;
+    if (a.dyn) {
+        uint64_t stat_steps = fair_steps * (100 - std::min<uint32_t>(ctx->dec_dyn_pct, 100)) / 100;
+        while (stat_steps && nwaves * stat_steps * step > nblocks) stat_steps--;
+        a.stat_blocks = stat_steps * step;
+        a.nstat = stat_steps ? (uint32_t)nwaves : 0;
+        a.range_blocks = dyn_steps * step;
+        const uint64_t ndyn = (nblocks - a.nstat * a.stat_blocks + a.range_blocks - 1) / a.range_blocks;
+        a.nranges = a.nstat + ndyn;
+        a.per_xcd = (uint32_t)((ndyn + kXcds - 1) / kXcds);
+    } else {
+        uint64_t range_steps = fair_steps;
+        if (a.sess_blocks) {
+            const uint64_t sess_steps = a.sess_blocks / step;
+            while (sess_steps % range_steps) range_steps--;
+        }
+        a.stat_blocks = a.range_blocks = range_steps * step;
+        a.nranges = (nblocks + a.stat_blocks - 1) / a.stat_blocks;
+        a.nstat = (uint32_t)std::min<uint64_t>(a.nranges, 0xFFFFFFFFull);
     }
-    a.range_blocks = range_steps * step;
-    a.nranges = (nblocks + a.range_blocks - 1) / a.range_blocks;
     if (a.nranges > 0xFFFFFFFFull) return CYAES_EINVAL;  // 32-bit tickets (> 2^40 blocks)
+    a.prio_short = fair_steps <= kDecShortSteps;
     a.bpp = make_fastdiv(bpp);
     a.step_q = (uint32_t)(step / bpp);
     a.step_r = (uint32_t)(step % bpp);
@@ -284,7 +311,6 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     st = work.get(ctx->pool, 4ull * ww, stream);
     if (st) return st;
     a.work = static_cast<uint32_t*>(work.p);
-    a.per_wg = (uint32_t)((a.nranges + grid - 1) / grid);
     if (in == out && a.nranges > 1) {
         st = boundary.get(ctx->pool, a.nranges * sizeof(uint4), stream);
         if (st) return st;
@@ -322,7 +348,7 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     // the waves finish; static: >= 2), up to 64 (one holder lane each); small
     // payloads then share rows.  Sweeps in profiles/r01/ab_ragged_groups.txt, r04.
     const uint64_t slots = (uint64_t)std::max(1, ctx->num_cus) * (kDecThreads / 64);
-    const uint64_t per_wave = ctx->dec_dyn ? std::max<uint32_t>(1, ctx->dec_groups_per_wave) : 2;
+    const uint64_t per_wave = ctx->dec_dyn == 1 ? std::max<uint32_t>(1, ctx->dec_groups_per_wave) : 2;
     const uint64_t G = ctx->ragged_group ? ctx->ragged_group
                                          : std::min<uint64_t>(64, std::max<uint64_t>(1, npayloads / (per_wave * slots)));
     a.group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, G));
@@ -330,13 +356,20 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     if (a.nranges > 0xFFFFFFFFull) return CYAES_EINVAL;  // 32-bit tickets
     const Shape sh = wave_shape(ctx, a.nranges, kDecThreads);
     const int grid = std::min(sh.grid, dec_grid_cap(ctx));
-    a.dyn = ctx->dec_dyn && a.nranges > (uint64_t)grid * (sh.threads / 64);  // more groups than waves
+    // Groups [0, nstat) static (strided over the waves), the rest a dynamic pool
+    // from per-XCD ticket pools with stealing (as the flat kernel's ranges).
+    const uint64_t nwaves = (uint64_t)grid * (sh.threads / 64);
+    a.dyn = ctx->dec_dyn == 1 && a.nranges > nwaves;  // (off by default: no faster on relay streams, r04)
+    if (a.dyn) {
+        const uint64_t stat_per_wave = a.nranges * (100 - std::min<uint32_t>(ctx->dec_dyn_pct, 100)) / 100 / nwaves;
+        a.nstat = (uint32_t)(stat_per_wave * nwaves);
+        a.per_xcd = (uint32_t)((a.nranges - a.nstat + kXcds - 1) / kXcds);
+    }
     StreamScratch work;
     const uint32_t ww = dec_work_words((uint32_t)grid);
     st = work.get(ctx->pool, 4ull * ww, stream);
     if (st) return st;
     a.work = static_cast<uint32_t*>(work.p);
-    a.per_wg = (uint32_t)((a.nranges + grid - 1) / grid);
     if (a.dyn) CY_TRY(launch_dec_prepass(a, ww, stream));
     return map_err(launch_decrypt_ragged(a, grid, sh.threads, stream));
 }
@@ -415,10 +448,11 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* g = getenv("CYAES_RAGGED_GROUP")) ctx->ragged_group = (uint32_t)strtoul(g, nullptr, 10);
     if (const char* r = getenv("CYAES_ENC_RUN")) ctx->enc_run = (uint32_t)strtoul(r, nullptr, 10);
     if (const char* v = getenv("CYAES_ENC_NO_SESS")) ctx->enc_no_sess = atoi(v) != 0;
-    if (const char* v = getenv("CYAES_DEC_DYN")) ctx->dec_dyn = atoi(v) != 0;
+    if (const char* v = getenv("CYAES_DEC_DYN")) ctx->dec_dyn = atoi(v) != 0 ? 1 : 0;
     if (const char* v = getenv("CYAES_DEC_RANGE_STEPS")) ctx->dec_range_steps = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_DEC_GROUPS_PER_WAVE")) ctx->dec_groups_per_wave = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_DEC_GRID")) ctx->dec_grid_max = atoi(v);
+    if (const char* v = getenv("CYAES_DEC_DYN_PCT")) ctx->dec_dyn_pct = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_STRIDED_LISTS")) ctx->strided_lists = atoi(v) != 0;
     const HostTables& t = host_tables();
     uint8_t host[kTablesBytes];
@@ -628,10 +662,11 @@ int cyaes_gpu_cbc_decrypt_batch(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_
                                     stream);
 }
 
-// Strided batches: the decrypt runs the flat kernel's STRIDED addressing when
-// it applies (unkeyed, >= 64 blocks per payload: the relay's MTU packets);
-// anything else, and every encrypt, runs as the ragged batch it is, with the
-// two lists written on the device first (12 B per payload).
+// Strided batches: the encrypt runs the ragged kernels with positions computed
+// from the stride; the decrypt runs the flat kernel's STRIDED addressing when
+// it applies (unkeyed, >= 64 blocks per payload: the relay's MTU packets), and
+// otherwise the ragged kernel with the two lists written on the device first
+// (12 B per payload; CYAES_STRIDED_LISTS=1 forces that for both, tests / A/B).
 static int strided_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* in, uint8_t* out, uint64_t first,
                          uint64_t stride, uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx,
                          uint32_t ppk, hipStream_t stream) {
@@ -645,6 +680,9 @@ static int strided_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* in, uint8_
         !ctx->strided_lists)
         return decrypt_uniform(ctx, in, out, npayloads, payload_bytes, nullptr, 0, nullptr, nullptr, stream, nullptr, 0,
                                first, stride);
+    if (!decrypt && !ctx->strided_lists)  // the ragged encrypt kernels compute the positions themselves
+        return encrypt_common(ctx, in, out, nullptr, nullptr, npayloads, payload_bytes, key_idx, ppk, nullptr, nullptr,
+                              stream, nullptr, 0, first, stride);
     StreamScratch lists;
     int st = lists.get(ctx->pool, npayloads * 12, stream);
     if (st) return st;

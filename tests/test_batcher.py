@@ -822,7 +822,7 @@ def test_device_relay_stream_strided(chunk, mode):
     relay_server.cpp:329)."""
     import numpy as np
     import torch
-    env = {"default": {}, "dyn1": {"CYAES_DEC_GRID": "3", "CYAES_DEC_RANGE_STEPS": "1"},
+    env = {"default": {}, "dyn1": {"CYAES_DEC_GRID": "3", "CYAES_DEC_RANGE_STEPS": "1", "CYAES_DEC_DYN": "1"},
            "lists": {"CYAES_STRIDED_LISTS": "1"}}[mode]
     key = _keys(1, 51)[0]
     rng = random.Random(51)

@@ -40,7 +40,8 @@ def torch():
 # runs the static per-wave split on a 2-workgroup grid.
 KERNEL_MODES = {"auto": {}, "lane": {"CYAES_QUAD_MAX_CHAINS": "0"},
                 "run3": {"CYAES_QUAD_MAX_CHAINS": "0", "CYAES_ENC_RUN": "3"},
-                "dyn1": {"CYAES_DEC_GRID": "3", "CYAES_DEC_RANGE_STEPS": "1", "CYAES_DEC_GROUPS_PER_WAVE": "64"},
+                "dyn1": {"CYAES_DEC_GRID": "3", "CYAES_DEC_RANGE_STEPS": "1", "CYAES_DEC_GROUPS_PER_WAVE": "64",
+                         "CYAES_DEC_DYN": "1"},
                 "static1": {"CYAES_QUAD_MAX_CHAINS": "0", "CYAES_DEC_GRID": "2", "CYAES_DEC_DYN": "0"}}
 _MODE_VARS = ("CYAES_QUAD_MAX_CHAINS", "CYAES_ENC_RUN", "CYAES_DEC_GRID", "CYAES_DEC_RANGE_STEPS",
               "CYAES_DEC_GROUPS_PER_WAVE", "CYAES_DEC_DYN")
@@ -262,7 +263,8 @@ def test_dynamic_ranges_full_grid(torch, pb, n, inplace):
     pt = oracle.synthetic(11, n, pb)
     ct = oracle.batch(False, [K0], 0, pt, pb, nthreads=16)
     outs = []
-    for env in ({}, {"CYAES_DEC_DYN": "0"}, {"CYAES_DEC_RANGE_STEPS": "1"}, {"CYAES_DEC_RANGE_STEPS": "5"}):
+    for env in ({}, {"CYAES_DEC_DYN": "0"}, {"CYAES_DEC_DYN": "1", "CYAES_DEC_RANGE_STEPS": "1"},
+                {"CYAES_DEC_DYN": "1", "CYAES_DEC_RANGE_STEPS": "5", "CYAES_DEC_DYN_PCT": "60"}):
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         c = ca.GpuContext(0)
@@ -307,6 +309,7 @@ def test_concurrent_flat_and_ragged_decrypts(torch):
         c.encrypt_uniform(flat, flat, n, pb, stream=a.cuda_stream)
         c.encrypt_ragged(rbuf, rbuf, off, nb, n, stream=b.cuda_stream)
         c.encrypt_uniform(flat2, flat2, n, pb, stream=b.cuda_stream)
+        torch.cuda.synchronize()  # the next rep swaps the streams: a buffer's ops stay ordered
     c.decrypt_uniform(flat, flat, n, pb, stream=s1.cuda_stream)
     c.decrypt_ragged(rbuf, rbuf, off, nb, n, stream=s2.cuda_stream)
     torch.cuda.synchronize()

@@ -77,7 +77,7 @@ def draw_case(seed):
              # decrypt work distribution: a small grid with 1- or 3-step ticket ranges, or the static split
              "CYAES_DEC_GRID": str(rng.choice([1, 2, 5])) if rng.integers(0, 2) else None,
              "CYAES_DEC_RANGE_STEPS": str(rng.choice([1, 3])) if rng.integers(0, 2) else None,
-             "CYAES_DEC_DYN": "0" if rng.integers(0, 4) == 0 else None})
+             "CYAES_DEC_DYN": str(rng.integers(0, 2)) if rng.integers(0, 3) else None})
 
 
 @pytest.mark.parametrize("seed", range(NCASES))
