@@ -219,7 +219,7 @@ void run(Looper* L, Clock::time_point until, uint64_t min_rounds) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    uint32_t threads = 8, pipes = 16, chunks = 256, batch_mb = 32, delay_us = 100, recv_copy = 1, verify = 1, depth = 2;
+    uint32_t threads = 8, pipes = 16, chunks = 256, batch_mb = 32, delay_us = 100, recv_copy = 1, verify = 1, depth = 4;
     std::string size_arg = "1472";
     double seconds = 4;
     for (int i = 1; i + 1 < argc; i += 2) {
