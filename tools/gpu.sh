@@ -7,6 +7,7 @@
 #   test       python -m pytest tests -m gpu (product build)
 #   bounds     the same suite on the bounds-checked build (CYAES_LIBRARY=build/variants/bounds.so)
 #   smoke      __graft_entry__.smoke()
+#   soak       tests/test_gpu_sweep.py with CYAES_SWEEP_CASES=${SOAK:-2000}
 #   bench      python bench.py (default: config E headline + packet configs + relay stream)
 #   quickbench bench.py --steps 3 --warmup 1 (no CPU baseline)
 #   profile    rocprofv3 --kernel-trace --stats of a short bench, then FETCH_SIZE / WRITE_SIZE PMC passes
@@ -45,6 +46,7 @@ for step in "$@"; do
     test) run pytest_gpu 600 $PYT ;;
     bounds) CYAES_LIBRARY=$R/build/variants/bounds.so run pytest_bounds 600 $PYT ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    soak) CYAES_SWEEP_CASES=${SOAK:-2000} run sweep_soak 900 python -u -m pytest tests/test_gpu_sweep.py -m gpu -x -q --timeout 600 --timeout-method thread ;;
     bench) run bench 400 python bench.py ;;
     quickbench) run quickbench 300 python bench.py --steps 3 --warmup 1 --no-cpu ;;
     profile)
