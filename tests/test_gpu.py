@@ -259,12 +259,15 @@ def test_dynamic_ranges_full_grid(torch, pb, n, inplace):
     VERDICT r03 next 2): MTU payloads (!BIG rows), 64 KiB payloads (one payload
     start per step at most), and a payload size that does not divide a step.
     In place, every range's C[begin-1] comes from the prepass snapshot.  The
-    same batch under the static per-wave split gives the same bytes."""
+    same batch under the static per-wave split gives the same bytes.  An
+    all-dynamic split of one-step ranges makes waves prefetch the first step
+    of their next range often, next to the batch's partial last range."""
     pt = oracle.synthetic(11, n, pb)
     ct = oracle.batch(False, [K0], 0, pt, pb, nthreads=16)
     outs = []
     for env in ({}, {"CYAES_DEC_DYN": "0"}, {"CYAES_DEC_DYN": "1", "CYAES_DEC_RANGE_STEPS": "1"},
-                {"CYAES_DEC_DYN": "1", "CYAES_DEC_RANGE_STEPS": "5", "CYAES_DEC_DYN_PCT": "60"}):
+                {"CYAES_DEC_DYN": "1", "CYAES_DEC_RANGE_STEPS": "5", "CYAES_DEC_DYN_PCT": "60"},
+                {"CYAES_DEC_DYN": "1", "CYAES_DEC_RANGE_STEPS": "1", "CYAES_DEC_DYN_PCT": "100"}):
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         c = ca.GpuContext(0)
