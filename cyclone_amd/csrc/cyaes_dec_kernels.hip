@@ -46,11 +46,6 @@ __device__ __forceinline__ void flat_position(const DecArgs& a, FlatPos ps, uint
 __device__ __forceinline__ uint64_t soff(const DecArgs& a, uint64_t p, uint32_t r) {
     return a.off0 + p * a.stride + 16ull * r;
 }
-// The same without off0 (folded into the range's base pointers) for 32-bit
-// payload indices: one v_mad_u64_u32 per row.
-__device__ __forceinline__ uint64_t soff32(uint32_t stride, uint32_t p, uint32_t r) {
-    return (uint64_t)p * stride + 16u * r;
-}
 __device__ __forceinline__ uint64_t soff_g(const DecArgs& a, uint64_t g) {  // flat block g (partial steps only)
     const uint64_t p = g / a.bpp.d;
     return soff(a, p, (uint32_t)(g - p * a.bpp.d));
@@ -58,37 +53,43 @@ __device__ __forceinline__ uint64_t soff_g(const DecArgs& a, uint64_t g) {  // f
 __device__ __forceinline__ Ext data_ext(const uint8_t* base, const DecArgs& a, bool strided) {
     return strided ? ext(base + a.off0, (a.npayloads - 1) * a.stride + 16ull * a.bpp.d) : ext(base, 16 * a.nblocks);
 }
-// Position (r, p) of row k's block in a STRIDED !BIG full step, from row 0's
-// (rk[0], pk[0]): rows are 64 blocks apart and payloads >= 64 blocks (the
-// runtime's condition for STRIDED), so each row wraps at most once.  Only row
-// 0's position is carried across steps: two VGPRs, where tracking every row
-// took eight and the step loop lost its schedule at the 128-VGPR limit.
-__device__ __forceinline__ void srow_pos(uint32_t bpp, int k, const uint32_t (&rk)[kDecRows],
-                                         const uint32_t (&pk)[kDecRows], uint32_t& r, uint32_t& p) {
+// Position r of row k's block in its payload in a STRIDED !BIG full step, and
+// the row's byte offset o (from in + off0), from row 0's (rk[0], pk[0] = its
+// offset): rows are 64 blocks apart and payloads >= 64 blocks (the runtime's
+// condition for STRIDED), so each row wraps at most once, and each wrap skips
+// the gap between payloads (stride - payload bytes).  Only row 0's position
+// is carried across steps: two VGPRs, where tracking every row took eight and
+// the step loop lost its schedule at the 128-VGPR limit.
+__device__ __forceinline__ void srow_pos(uint32_t bpp, uint32_t gap, int k, const uint32_t (&rk)[kDecRows],
+                                         const uint32_t (&pk)[kDecRows], uint32_t& r, uint32_t& o) {
     r = rk[0];
-    p = pk[0];
+    o = pk[0] + 1024u * k;
     for (int j = 0; j < k; j++) {
         const uint32_t t = r + 64;
         const bool wrap = t >= bpp;
         r = wrap ? t - bpp : t;
-        p += wrap ? 1u : 0u;
+        o += wrap ? gap : 0u;
     }
 }
 // Byte offset (from in + off0) of row k's block in a STRIDED full step: !BIG
-// from row 0's tracked position, BIG from the step position (at most one
-// payload start).
+// from row 0's tracked offset, BIG from the step position (at most one payload
+// start).  32-bit: the runtime runs this kernel only on streams that span less
+// than 4 GiB, so the loads and stores take the scalar base + 32-bit lane
+// offset form.  (With 64-bit per-row address arithmetic on both the loads and
+// the stores, the step lost its schedule: 315 s_waitcnt per 640 LDS reads
+// against 53.)
 template <bool BIG>
-__device__ __forceinline__ uint64_t srow(const DecArgs& a, FlatPos ps, uint32_t lane, int k, const uint32_t (&rk)[kDecRows],
+__device__ __forceinline__ uint32_t srow(const DecArgs& a, FlatPos ps, uint32_t lane, int k, const uint32_t (&rk)[kDecRows],
                                          const uint32_t (&pk)[kDecRows]) {
-    const uint32_t stride = (uint32_t)a.stride;  // (the runtime keeps strides and payload indices 32-bit)
+    const uint32_t stride = (uint32_t)a.stride;
     if (BIG) {
         const uint32_t lpos = ps.bpos + 64 * k + lane;
         const bool next = lpos >= a.bpp.d;
-        return soff32(stride, (uint32_t)ps.bp + (next ? 1u : 0u), next ? lpos - a.bpp.d : lpos);
+        return (uint32_t)ps.bp * stride + (next ? stride - 16u * a.bpp.d : 0u) + 16u * lpos;
     }
-    uint32_t r, p;
-    srow_pos(a.bpp.d, k, rk, pk, r, p);
-    return soff32(stride, p, r);
+    uint32_t r, o;
+    srow_pos(a.bpp.d, stride - 16u * a.bpp.d, k, rk, pk, r, o);
+    return o;
 }
 
 // Loads the R rows of the step at `base` (c); partial steps also load each
@@ -171,8 +172,8 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
     } else if (!IV || !a.iv_in) {  // chains restart at DefaultIV: a select on the lane's tracked position
 #pragma unroll
         for (int k = 0; k < R; k++) {
-            uint32_t r = rk[k], p;
-            if (STRIDED) srow_pos(a.bpp.d, k, rk, pk, r, p);
+            uint32_t r = rk[k], o;
+            if (STRIDED) srow_pos(a.bpp.d, 0u, k, rk, pk, r, o);
             if (r == 0) pv[k] = default_iv();
         }
     } else {
@@ -352,18 +353,24 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
                 const Fastdiv bd = {ka->bpp.M, ka->bpp.d};
                 const uint32_t q = fastdiv(lpos, bd);
                 rk[k] = lpos - q * bd.d;
-                if (STRIDED) pk[k] = (uint32_t)ps.bp + q;
+                if (STRIDED) pk[k] = (uint32_t)(ps.bp + q) * (uint32_t)ka->stride + 16u * rk[k];  // row 0's offset
             }
         }
         auto advance = [&] {
             ps.bpos += a.step_r;
             ps.bp += a.step_q;
             if (ps.bpos >= a.bpp.d) { ps.bpos -= a.bpp.d; ps.bp++; }
+            if (STRIDED) {  // wave-uniform: keep it in SGPRs (the compiler moved it to a VGPR pair)
+                ps.bp = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ps.bp >> 32)) << 32) |
+                        __builtin_amdgcn_readfirstlane((uint32_t)ps.bp);
+                ps.bpos = __builtin_amdgcn_readfirstlane(ps.bpos);
+            }
             if (!BIG) {
 #pragma unroll
                 for (int k = 0; k < (STRIDED ? 1 : R); k++) {
                     const uint32_t t = rk[k] + a.step_r;  // < 2 bpp
-                    if (STRIDED) pk[k] += a.step_q + (t >= a.bpp.d ? 1u : 0u);
+                    if (STRIDED)  // 64 R blocks on, and the gap of each payload start passed
+                        pk[k] += 1024u * R + (a.step_q + (t >= a.bpp.d ? 1u : 0u)) * ((uint32_t)a.stride - 16u * a.bpp.d);
                     rk[k] = min(t, t - a.bpp.d);
                 }
             }

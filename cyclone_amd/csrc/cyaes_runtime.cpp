@@ -676,8 +676,9 @@ static int strided_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* in, uint8_
     if (npayloads - 1 > (UINT64_MAX - first - payload_bytes) / stride) return CYAES_EINVAL;
     DeviceGuard g(ctx->device);
     const uint32_t bpp = payload_bytes / 16;
-    if (decrypt && !key_idx && !ppk && bpp >= 64 && npayloads <= 0xFFFFFFFFull && stride <= 0xFFFFFFFFull &&
-        !ctx->strided_lists)
+    // The flat kernel's strided rows use 32-bit byte offsets from the stream's first payload
+    const bool span32 = (npayloads - 1) * stride + payload_bytes <= 0xFFFFFFFFull;
+    if (decrypt && !key_idx && !ppk && bpp >= 64 && span32 && !ctx->strided_lists)
         return decrypt_uniform(ctx, in, out, npayloads, payload_bytes, nullptr, 0, nullptr, nullptr, stream, nullptr, 0,
                                first, stride);
     if (!decrypt && !ctx->strided_lists)  // the ragged encrypt kernels compute the positions themselves
