@@ -37,10 +37,16 @@ struct cyaes_gpu {
     uint32_t* d_status = nullptr;
     unsigned long long* d_digest = nullptr;
     struct HostPipe* pipe = nullptr;  // cyaes_gpu_{en,de}crypt_host, created on first use
-    // Private stream-ordered pool for per-call scratch (StreamScratch).  Not the
-    // device's default pool: its policies and release threshold belong to every
-    // other user in the process (torch, RCCL).
-    hipMemPool_t pool = nullptr;
+    // Per-call scratch blocks (StreamScratch), cached for the context's life.
+    struct ScratchBlock {
+        void* p;
+        uint64_t bytes;
+        hipEvent_t done;  // recorded on the last user's stream behind its kernels
+        bool in_use;      // held by a call that is still enqueuing
+        bool pending;     // `done` recorded and not yet seen complete
+    };
+    std::mutex scratch_mu;
+    std::vector<ScratchBlock> scratch;
 };
 
 namespace {
@@ -196,22 +202,79 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     return map_err(launch_encrypt(a, sess ? (int)sess_grid : std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
 }
 
-// Per-call device scratch, stream-ordered (hipMallocFromPoolAsync /
-// hipFreeAsync on the batch's stream, from the context's private pool): batches
-// of one context on different streams never share a scratch buffer while a
-// kernel still reads it.  The pool never hands a block freed on one stream to
-// another stream opportunistically; reuse across streams only follows the
-// stream-order dependencies the runtime can see.
+// Per-call device scratch (the decrypt's work words and range-boundary
+// snapshots, IV copies, strided lists), stream-ordered by events: blocks come
+// from hipMalloc and stay cached in the context; releasing one records an
+// event on the batch's stream behind the kernels that use it, and a block is
+// handed out again only once its event has completed.  So batches of one
+// context on different streams never share a block while a kernel still
+// reads it, and nothing is freed before the context is destroyed.
+// (Until late r04 the blocks came from a private hipMemPool with
+// hipMallocFromPoolAsync / hipFreeAsync.  Twice in r04's GPU runs a torch
+// host-to-device copy right after one context was destroyed (its pool with
+// it) and the next created failed with an illegal address, with no kernel
+// of this library launched since a device-wide synchronisation: the pool's
+// deferred release is the suspect, so the library no longer uses the
+// stream-ordered allocator)
+constexpr size_t kScratchMaxBlocks = 64;  // beyond this, wait for a pending block instead of allocating
+
 struct StreamScratch {
     void* p = nullptr;
+    cyaes_gpu* ctx = nullptr;
+    size_t idx = 0;
     hipStream_t s = nullptr;
-    int get(hipMemPool_t pool, uint64_t bytes, hipStream_t stream) {
+    int get(cyaes_gpu* c, uint64_t bytes, hipStream_t stream) {
+        std::lock_guard<std::mutex> lk(c->scratch_mu);
+        auto& v = c->scratch;
+        size_t best = v.size(), oldest = v.size();
+        for (size_t i = 0; i < v.size(); i++) {
+            auto& b = v[i];
+            if (b.in_use || b.bytes < bytes) continue;
+            if (b.pending) {
+                const hipError_t q = hipEventQuery(b.done);
+                if (q == hipErrorNotReady) {
+                    if (oldest == v.size()) oldest = i;
+                    continue;
+                }
+                if (q != hipSuccess) return map_err(q);
+                b.pending = false;
+            }
+            if (best == v.size() || b.bytes < v[best].bytes) best = i;
+        }
+        if (best == v.size() && v.size() >= kScratchMaxBlocks && oldest != v.size()) {
+            CY_TRY(hipEventSynchronize(v[oldest].done));
+            v[oldest].pending = false;
+            best = oldest;
+        }
+        if (best == v.size()) {
+            uint64_t cap = 4096;
+            while (cap < bytes) cap *= 2;
+            void* mem = nullptr;
+            CY_TRY(hipMalloc(&mem, cap));
+            hipEvent_t ev = nullptr;
+            const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+            if (e != hipSuccess) {
+                (void)hipFree(mem);
+                return map_err(e);
+            }
+            v.push_back({mem, cap, ev, false, false});
+            best = v.size() - 1;
+        }
+        v[best].in_use = true;
+        p = v[best].p;
+        ctx = c;
+        idx = best;
         s = stream;
-        CY_TRY(hipMallocFromPoolAsync(&p, bytes, pool, stream));
         return CYAES_OK;
     }
     ~StreamScratch() {
-        if (p) (void)hipFreeAsync(p, s);  // after the kernels queued on s
+        if (!p) return;
+        std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+        auto& b = ctx->scratch[idx];
+        // after the kernels queued on s; if the record fails, the block stays
+        // out of use until the context is destroyed (its synchronisation)
+        b.pending = hipEventRecord(b.done, s) == hipSuccess;
+        b.in_use = !b.pending;
     }
 };
 
@@ -220,7 +283,7 @@ struct StreamScratch {
 int alias_iv(cyaes_gpu* ctx, StreamScratch& sc, const uint8_t** iv_in, const uint8_t* iv_out, uint64_t npayloads,
              hipStream_t stream) {
     if (!*iv_in || *iv_in != iv_out) return CYAES_OK;
-    int st = sc.get(ctx->pool, npayloads * 16, stream);
+    int st = sc.get(ctx, npayloads * 16, stream);
     if (st) return st;
     CY_TRY(hipMemcpyAsync(sc.p, *iv_in, npayloads * 16, hipMemcpyDeviceToDevice, stream));
     *iv_in = static_cast<const uint8_t*>(sc.p);
@@ -308,11 +371,11 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     a.status = ctx->d_status;
     a.inplace = in == out;
     const uint32_t ww = dec_work_words((uint32_t)grid);
-    st = work.get(ctx->pool, 4ull * ww, stream);
+    st = work.get(ctx, 4ull * ww, stream);
     if (st) return st;
     a.work = static_cast<uint32_t*>(work.p);
     if (in == out && a.nranges > 1) {
-        st = boundary.get(ctx->pool, a.nranges * sizeof(uint4), stream);
+        st = boundary.get(ctx, a.nranges * sizeof(uint4), stream);
         if (st) return st;
         a.boundary = static_cast<uint4*>(boundary.p);
     }
@@ -367,7 +430,7 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     }
     StreamScratch work;
     const uint32_t ww = dec_work_words((uint32_t)grid);
-    st = work.get(ctx->pool, 4ull * ww, stream);
+    st = work.get(ctx, 4ull * ww, stream);
     if (st) return st;
     a.work = static_cast<uint32_t*>(work.p);
     if (a.dyn) CY_TRY(launch_dec_prepass(a, ww, stream));
@@ -464,20 +527,6 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_status), 16);
     if (e == hipSuccess) e = hipMemset(ctx->d_status, 0, 16);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_digest), 16);
-    if (e == hipSuccess) {
-        // Per-call scratch (StreamScratch): a private pool, kept warm up to 64
-        // MiB across synchronisations, with no opportunistic cross-stream reuse.
-        hipMemPoolProps props = {};
-        props.allocType = hipMemAllocationTypePinned;
-        props.handleTypes = hipMemHandleTypeNone;
-        props.location.type = hipMemLocationTypeDevice;
-        props.location.id = device;
-        e = hipMemPoolCreate(&ctx->pool, &props);
-        uint64_t keep = 64ull << 20;
-        int no = 0;
-        if (e == hipSuccess) e = hipMemPoolSetAttribute(ctx->pool, hipMemPoolAttrReleaseThreshold, &keep);
-        if (e == hipSuccess) e = hipMemPoolSetAttribute(ctx->pool, hipMemPoolReuseAllowOpportunistic, &no);
-    }
     if (e != hipSuccess) {
         cyaes_gpu_destroy(ctx);
         return map_err(e);
@@ -498,7 +547,10 @@ int cyaes_gpu_destroy(cyaes_gpu* ctx) {
     (void)hipFree(ctx->d_status);
     (void)hipFree(ctx->d_digest);
     destroy_pipe(ctx->pipe);
-    if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);
+    for (auto& b : ctx->scratch) {  // (every batch has completed: the synchronisation above)
+        (void)hipFree(b.p);
+        (void)hipEventDestroy(b.done);
+    }
     delete ctx;
     return map_err(e);
 }
@@ -685,7 +737,7 @@ static int strided_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* in, uint8_
         return encrypt_common(ctx, in, out, nullptr, nullptr, npayloads, payload_bytes, key_idx, ppk, nullptr, nullptr,
                               stream, nullptr, 0, first, stride);
     StreamScratch lists;
-    int st = lists.get(ctx->pool, npayloads * 12, stream);
+    int st = lists.get(ctx, npayloads * 12, stream);
     if (st) return st;
     uint64_t* offs = static_cast<uint64_t*>(lists.p);
     uint32_t* nb = reinterpret_cast<uint32_t*>(offs + npayloads);
@@ -752,13 +804,13 @@ int cyaes_gpu_digest(const uint8_t* d_buf, uint64_t nbytes, uint64_t out[2], voi
     if (!out || nbytes % 8 || (nbytes && !d_buf)) return CYAES_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     unsigned long long* d_out = nullptr;
-    CY_TRY(hipMallocAsync(reinterpret_cast<void**>(&d_out), 16, s));
+    CY_TRY(hipMalloc(reinterpret_cast<void**>(&d_out), 16));
     hipError_t e = hipMemsetAsync(d_out, 0, 16, s);
     if (e == hipSuccess && nbytes) e = launch_digest(d_buf, nbytes / 8, d_out, s);
     unsigned long long h[2] = {0, 0};
     if (e == hipSuccess) e = hipMemcpyAsync(h, d_out, 16, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    (void)hipFreeAsync(d_out, s);
+    (void)hipFree(d_out);
     if (e != hipSuccess) return map_err(e);
     out[0] = h[0];
     out[1] = h[1];

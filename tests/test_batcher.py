@@ -863,6 +863,38 @@ def test_device_relay_stream_strided(chunk, mode):
     ctx.close()
 
 
+def test_strided_stream_beyond_4gib():
+    """A strided stream spanning more than 4 GiB (three 2,048-B payloads 2 GiB
+    + 16 B apart): the flat decrypt's strided rows use 32-bit offsets, so the
+    runtime sends such a stream through the list path; encrypt and decrypt in
+    place stay bit-exact and the bytes between payloads are untouched."""
+    import numpy as np
+    import torch
+    n, pb, stride, first = 3, 2048, (1 << 31) + 16, 12
+    key = _keys(1, 71)[0]
+    rng = np.random.default_rng(71)
+    plain = [rng.integers(0, 256, pb, dtype=np.uint8) for _ in range(n)]
+    ct = [np.frombuffer(bytes(oracle.Rijndael(key).encrypt(bytearray(x.tobytes()))), np.uint8) for x in plain]
+    size = first + (n - 1) * stride + pb + 64
+    buf = torch.full((size,), 0xA5, dtype=torch.uint8, device="cuda")
+    offs = [first + p * stride for p in range(n)]
+    for o, x in zip(offs, plain):
+        buf[o:o + pb] = torch.from_numpy(x).cuda()
+    ctx = ca.GpuContext(0)
+    ctx.set_keys(key)
+    ctx.encrypt_strided(buf, buf, first, stride, n, pb)
+    for o, x in zip(offs, ct):
+        assert np.array_equal(buf[o:o + pb].cpu().numpy(), x)
+    ctx.decrypt_strided(buf, buf, first, stride, n, pb)
+    for o, x in zip(offs, plain):
+        assert np.array_equal(buf[o:o + pb].cpu().numpy(), x)
+        assert int((buf[o - 12:o] != 0xA5).sum()) == 0 and int((buf[o + pb:o + pb + 12] != 0xA5).sum()) == 0
+    assert ctx.check() == ca.CYAES_OK
+    ctx.close()
+    del buf
+    torch.cuda.empty_cache()
+
+
 def test_strided_batch_session_keys():
     """Strided batches with per-session keys (payloads_per_key and a key index
     array) run as ragged batches with lists written on the device; the bytes
