@@ -728,6 +728,12 @@ static int strided_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* in, uint8_
     if (npayloads - 1 > (UINT64_MAX - first - payload_bytes) / stride) return CYAES_EINVAL;
     DeviceGuard g(ctx->device);
     const uint32_t bpp = payload_bytes / 16;
+    // Back-to-back payloads, 16-B aligned: a contiguous uniform batch
+    if (stride == payload_bytes && batch_args_ok(ctx, in + first, out + first, nullptr, nullptr))
+        return decrypt ? decrypt_uniform(ctx, in + first, out + first, npayloads, payload_bytes, key_idx, ppk, nullptr,
+                                         nullptr, stream)
+                       : encrypt_common(ctx, in + first, out + first, nullptr, nullptr, npayloads, payload_bytes,
+                                        key_idx, ppk, nullptr, nullptr, stream);
     // The flat kernel's strided rows use 32-bit byte offsets from the stream's first payload
     const bool span32 = (npayloads - 1) * stride + payload_bytes <= 0xFFFFFFFFull;
     if (decrypt && !key_idx && !ppk && bpp >= 64 && span32 && !ctx->strided_lists)

@@ -134,7 +134,10 @@ int cyaes_gpu_decrypt_ragged(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out
  *                 the two lists: the relay server's received stream of MTU
  *                 packets, payload at packet offset 12, stride = packet size
  *                 (relay_server.cpp:329; cyaes_relay_stride finds it).  No IV
- *                 arrays (the relay passes iv = nullptr). */
+ *                 arrays (the relay passes iv = nullptr).  Kernel choice (results
+ *                 identical): back-to-back 16-B aligned payloads run as a uniform
+ *                 batch; unkeyed decrypts of >= 64-block payloads spanning < 4 GiB
+ *                 run the flat decrypt's strided rows; the rest the ragged kernels. */
 int cyaes_gpu_encrypt_strided(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_out, uint64_t first_offset,
                               uint64_t stride, uint64_t npayloads, uint32_t payload_bytes, const uint32_t* d_key_idx,
                               uint32_t payloads_per_key, void* stream);

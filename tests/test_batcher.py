@@ -895,6 +895,34 @@ def test_strided_stream_beyond_4gib():
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("first", [0, 16, 12])
+def test_strided_contiguous_stream(first):
+    """A strided stream whose payloads lie back to back (stride = payload
+    bytes): at a 16-B aligned start it runs as a contiguous uniform batch,
+    per-session keys included; at a 4-B aligned one through the strided path.
+    Bit-exact against the oracle either way, bytes around the stream untouched."""
+    import numpy as np
+    import torch
+    n, pb, ppk = 257, 1472, 16
+    keys = _keys((n - 1) // ppk + 1, 81)
+    rng = np.random.default_rng(81)
+    plain = rng.integers(0, 256, n * pb, dtype=np.uint8)
+    ct = np.concatenate([np.frombuffer(bytes(oracle.Rijndael(keys[p // ppk]).encrypt(
+        bytearray(plain[p * pb:(p + 1) * pb].tobytes()))), np.uint8) for p in range(n)])
+    ctx = ca.GpuContext(0)
+    ctx.set_keys(b"".join(keys))
+    buf = torch.full((first + n * pb + 32,), 0xA5, dtype=torch.uint8, device="cuda")
+    buf[first:first + n * pb] = torch.from_numpy(plain).cuda()
+    ctx.encrypt_strided(buf, buf, first, pb, n, pb, payloads_per_key=ppk)
+    got = buf.cpu().numpy()
+    assert np.array_equal(got[first:first + n * pb], ct)
+    assert (got[:first] == 0xA5).all() and (got[first + n * pb:] == 0xA5).all()
+    ctx.decrypt_strided(buf, buf, first, pb, n, pb, payloads_per_key=ppk)
+    assert np.array_equal(buf[first:first + n * pb].cpu().numpy(), plain)
+    assert ctx.check() == ca.CYAES_OK
+    ctx.close()
+
+
 def test_strided_batch_session_keys():
     """Strided batches with per-session keys (payloads_per_key and a key index
     array) run as ragged batches with lists written on the device; the bytes
