@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""tools/ab_relay_layout.py -- where ragged encrypt and decrypt lose time on relay streams.
+"""tools/ab_relay_layout.py -- where ragged / strided encrypt and decrypt lose time on relay streams.
 
-Times cyaes_gpu_encrypt_ragged, then cyaes_gpu_decrypt_ragged of its output
+Times cyaes_gpu_encrypt_ragged, then cyaes_gpu_decrypt_ragged of its output (--api strided:
+cyaes_gpu_{en,de}crypt_strided)
 (in place, or back into the source stream), on N equal payloads under layouts that differ in
 one property at a time: packet stride (payload + header bytes), payload offset
 inside the packet (12 = relay, 16 = 16-B aligned) and in place vs a separate
@@ -23,6 +24,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--lib", nargs="*", default=None)
     ap.add_argument("--layouts", default=None, help="comma-separated subset of the layout labels")
+    ap.add_argument("--api", choices=["ragged", "strided"], default="ragged",
+                    help="ragged entry points (device offset / size lists) or the strided ones")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -66,7 +69,10 @@ def main():
                     fill()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
-                ck.encrypt_ragged(src, dst, off, nb, n, stream=s.cuda_stream)
+                if args.api == "strided":
+                    ck.encrypt_strided(src, dst, hdr, stride, n, pb, stream=s.cuda_stream)
+                else:
+                    ck.encrypt_ragged(src, dst, off, nb, n, stream=s.cuda_stream)
                 e1.record(s)
                 torch.cuda.synchronize()
                 if r:
@@ -75,7 +81,10 @@ def main():
                 # decrypt the stream just encrypted: in place, or into the (plaintext) source stream
                 back = dst if inplace else src
                 e0.record(s)
-                ck.decrypt_ragged(dst, back, off, nb, n, stream=s.cuda_stream)
+                if args.api == "strided":
+                    ck.decrypt_strided(dst, back, hdr, stride, n, pb, stream=s.cuda_stream)
+                else:
+                    ck.decrypt_ragged(dst, back, off, nb, n, stream=s.cuda_stream)
                 e1.record(s)
                 torch.cuda.synchronize()
                 if r:
