@@ -215,7 +215,7 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
 // it) and the next created failed with an illegal address, with no kernel
 // of this library launched since a device-wide synchronisation: the pool's
 // deferred release is the suspect, so the library no longer uses the
-// stream-ordered allocator, DESIGN.md §4.1.)
+// stream-ordered allocator, DESIGN.md §4.2.)
 constexpr size_t kScratchMaxBlocks = 64;  // beyond this, wait for a pending block instead of allocating
 
 struct StreamScratch {
