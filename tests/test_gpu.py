@@ -283,6 +283,32 @@ def test_dynamic_ranges_full_grid(torch, pb, n, inplace):
         assert np.array_equal(o, pt)
 
 
+def test_context_cycles_with_torch_copies(torch):
+    """Contexts created and destroyed back to back, each running in-place
+    decrypts (work words and boundary snapshots from its scratch blocks) and
+    an aliased-IV decrypt, with torch allocations and host-to-device copies
+    in between: the pattern around r04's two illegal-address reports, which
+    came from a torch copy right after a context and its stream-ordered
+    scratch pool were destroyed.  Bit-exact every cycle."""
+    n, pb = 96, 1472
+    pt = oracle.synthetic(31, n, pb)
+    ct = oracle.batch(False, [K0], 0, pt, pb, nthreads=4)
+    last = ct.reshape(n, pb // 16, 16)[:, -1].copy()
+    for cycle in range(120):
+        c = ca.GpuContext(0)
+        c.set_keys(K0)
+        d = dev(torch, ct)
+        c.decrypt_uniform(d, d, n, pb)
+        ivs = dev(torch, np.zeros((n, 16), np.uint8))
+        c.decrypt_uniform(dev(torch, ct), empty(torch, ct.size), n, pb, iv_in=ivs, iv_out=ivs)
+        junk = dev(torch, np.full(1 << 20, cycle & 0xFF, np.uint8))  # torch's allocator and copies in between
+        assert np.array_equal(host(d), pt), cycle
+        assert np.array_equal(host(ivs).reshape(n, 16), last), cycle
+        assert c.check() == ca.CYAES_OK
+        c.close()
+        del d, ivs, junk
+
+
 def test_concurrent_flat_and_ragged_decrypts(torch):
     """A flat and a ragged decrypt (and two flat ones) on two streams at once,
     repeatedly: each launch has its own ticket counter and progress words
