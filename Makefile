@@ -34,7 +34,7 @@ SCHED_ENC:= -mllvm -amdgpu-sched-strategy=iterative-ilp
 SCHED_DEC:= -mllvm -amdgpu-sched-strategy=max-ilp
 ASRC     := cyclone_amd/csrc/cyaes_adler.hip
 BSRC     := cyclone_amd/csrc/cyaes_batch_kernels.hip
-HSRC     := cyclone_amd/csrc/cyaes_runtime.cpp cyclone_amd/csrc/cyaes_tables.cpp cyclone_amd/csrc/cyr_rijndael.cpp \
+HSRC     := cyclone_amd/csrc/cyaes_runtime.cpp cyclone_amd/csrc/cyaes_pins.cpp cyclone_amd/csrc/cyaes_tables.cpp cyclone_amd/csrc/cyr_rijndael.cpp \
             cyclone_amd/csrc/cyaes_relay.cpp cyclone_amd/csrc/cyaes_batcher.cpp
 HDRS     := include/cyaes.h include/cyaes_relay.h include/cyaes_batch.h include/cyclone_amd/cyr_rijndael.h cyclone_amd/csrc/cyaes_internal.h \
             cyclone_amd/csrc/cyaes_tables.h

@@ -92,6 +92,7 @@ _SIGS = {
     "cyaes_gpu_update_keys": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32]),
     "cyaes_gpu_cbc_encrypt_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "cyaes_gpu_cbc_decrypt_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
+    "cyaes_debug_pins": (ctypes.c_int, [_u64p]),
     # include/cyaes_relay.h
     "cyaes_relay_round16": (ctypes.c_uint32, [ctypes.c_uint32]),
     "cyaes_relay_packet_bytes": (ctypes.c_uint32, [ctypes.c_uint32]),
@@ -178,6 +179,17 @@ def version():
 def _check(status, what):
     if status != CYAES_OK:
         raise CyaesError(status, what)
+
+
+PIN_FIELDS = ("live", "live_bytes", "registered", "unregistered", "failed_unregisters", "stale", "conflicts",
+              "refs")
+
+
+def debug_pins():
+    """The library's host-memory registrations (cyaes_debug_pins, include/cyaes.h)."""
+    out = (ctypes.c_uint64 * 8)()
+    _check(load_library().cyaes_debug_pins(out), "cyaes_debug_pins")
+    return dict(zip(PIN_FIELDS, (int(v) for v in out)))
 
 
 def key_expand(key):
@@ -311,6 +323,14 @@ class GpuContext:
             raise ValueError("keys must be a non-empty multiple of 16 bytes")
         buf = (ctypes.c_uint8 * len(keys)).from_buffer_copy(keys)
         _check(self._lib.cyaes_gpu_set_keys(self._h, ctypes.addressof(buf), len(keys) // 16), "set_keys")
+
+    def update_keys(self, first, keys):
+        """Replaces / appends rows [first, first + len(keys) / 16) (cyaes_gpu_update_keys)."""
+        keys = bytes(keys)
+        if not keys or len(keys) % 16:
+            raise ValueError("keys must be a non-empty multiple of 16 bytes")
+        buf = (ctypes.c_uint8 * len(keys)).from_buffer_copy(keys)
+        _check(self._lib.cyaes_gpu_update_keys(self._h, first, ctypes.addressof(buf), len(keys) // 16), "update_keys")
 
     def set_keys_device(self, d_keys, nkeys, stream=None):
         _check(self._lib.cyaes_gpu_set_keys_device(self._h, _p(d_keys), nkeys, _p(stream)), "set_keys_device")

@@ -197,14 +197,6 @@ struct PoolEnt {
     bool live = false;
 };
 
-// A page-aligned host range this batcher pinned (hipHostRegister).  Pools
-// whose pages overlap share it: two pools may sit on one page (two buffers of
-// one heap), so a range is unpinned only when no live pool uses it any more.
-struct PinEnt {
-    uintptr_t lo = 0, hi = 0;
-    uint32_t refs = 0;
-};
-
 // Per-thread snapshot of a batcher's session rows and pools, refreshed when
 // either table's version changes, so a submit takes no shared lock.
 std::atomic<uint64_t> g_batcher_ids{1};
@@ -300,8 +292,9 @@ struct cyaes_batcher {
     // Pools.
     std::mutex pmu;
     std::array<PoolEnt, kMaxPools> pools{};
-    std::array<std::vector<size_t>, kMaxPools> pool_pins;  // pool id -> the PinEnts (indices) it holds
-    std::vector<PinEnt> pins;                                // refs == 0: free entry
+    // pool id -> the registrations holding its pages (cyaes_pins.cpp: shared
+    // with other pools, of this batcher or another, that sit on the same pages)
+    std::array<cyaes::PinHold, kMaxPools> pool_pins;
     std::atomic<uint64_t> pools_version{1};
 
     const uint64_t id = g_batcher_ids.fetch_add(1);
@@ -909,8 +902,7 @@ void cyaes_batcher_destroy(cyaes_batcher* b) {
     }
     if (b->d_keys) (void)hipFree(b->d_keys);
     if (b->pipe) (void)hipStreamDestroy(b->pipe);
-    for (const PinEnt& p : b->pins)
-        if (p.refs) (void)hipHostUnregister(reinterpret_cast<void*>(p.lo));
+    for (cyaes::PinHold& h : b->pool_pins) (void)cyaes::pin_release(&h);  // pools the caller left registered
     (void)hipSetDevice(dev_prev);
     (void)cyaes_gpu_destroy(b->ctx);
     delete b;
@@ -979,92 +971,6 @@ int cyaes_batcher_session_close(cyaes_batcher* b, uint32_t slot) {
     return CYAES_OK;
 }
 
-// Pins [lo, hi) for a new pool (pmu held, the batcher's device current):
-// pages already pinned by this batcher are shared, the rest are registered
-// here; a range some other owner registered (hipHostMalloc, the caller's own
-// hipHostRegister) is used only if that one registration covers it.  On
-// success `held` lists the PinEnts covering the range, one ref taken on each
-// (unpin() returns them); on failure nothing stays registered.
-static int pin_span(cyaes_batcher* b, uintptr_t lo, uintptr_t hi, std::vector<size_t>* held) {
-    std::vector<std::pair<uintptr_t, uintptr_t>> gaps;  // pages not pinned by this batcher
-    std::vector<size_t> ours;
-    for (size_t i = 0; i < b->pins.size(); i++)
-        if (b->pins[i].refs && b->pins[i].lo < hi && lo < b->pins[i].hi) ours.push_back(i);
-    std::sort(ours.begin(), ours.end(), [&](size_t x, size_t y) { return b->pins[x].lo < b->pins[y].lo; });
-    uintptr_t c = lo;
-    for (size_t i : ours) {
-        if (b->pins[i].lo > c) gaps.push_back({c, b->pins[i].lo});
-        c = std::max(c, b->pins[i].hi);
-    }
-    if (c < hi) gaps.push_back({c, hi});
-    std::vector<PinEnt> added;
-    auto rollback = [&] {
-        for (const PinEnt& p : added) (void)hipHostUnregister(reinterpret_cast<void*>(p.lo));
-        (void)hipGetLastError();
-    };
-    // The registration holding page q, if one does: its base as
-    // hipMemGetAddressRange reports it (the registration's DEVICE range, not
-    // the host one: tools/hostreg_probe.hip, profiles/r04/hostreg_probe.txt),
-    // only compared between pages here.
-    auto registration = [](uintptr_t q, uintptr_t* base) {
-        hipDeviceptr_t rb = nullptr;
-        size_t rs = 0;
-        if (hipMemGetAddressRange(&rb, &rs, reinterpret_cast<hipDeviceptr_t>(q)) != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-        }
-        *base = (uintptr_t)rb;
-        return true;
-    };
-    for (const auto& g : gaps) {
-        // Pages someone else registered (hipHostMalloc, the caller's own
-        // hipHostRegister): one such registration must hold every page of the
-        // gap, and is then used as it is.  Never register over part of another
-        // owner's registration: HIP accepts the overlapping range, but
-        // unregistering either one corrupts the other's record (measured: the
-        // other owner's hipHostUnregister fails afterwards).  Checked page by page.
-        uintptr_t rb0 = 0, rb = 0;
-        if (registration(g.first, &rb0)) {
-            for (uintptr_t q = g.first + 4096; q < g.second; q += 4096)
-                if (!registration(q, &rb) || rb != rb0) {
-                    rollback();
-                    return CYAES_EINVAL;
-                }
-            continue;
-        }
-        for (uintptr_t q = g.first + 4096; q < g.second; q += 4096)
-            if (registration(q, &rb)) {
-                rollback();
-                return CYAES_EINVAL;
-            }
-        void* a = reinterpret_cast<void*>(g.first);
-        const hipError_t e = hipHostRegister(a, g.second - g.first, hipHostRegisterMapped);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            rollback();
-            return map_err(e);
-        }
-        added.push_back(PinEnt{g.first, g.second, 0});
-    }
-    for (size_t i : ours) b->pins[i].refs++;
-    for (const PinEnt& p : added) {
-        size_t i = 0;
-        while (i < b->pins.size() && b->pins[i].refs) i++;
-        if (i == b->pins.size()) b->pins.push_back(p);
-        else b->pins[i] = p;
-        b->pins[i].refs = 1;
-        ours.push_back(i);
-    }
-    *held = ours;
-    return CYAES_OK;
-}
-
-static void unpin(cyaes_batcher* b, const std::vector<size_t>& held) {
-    for (size_t i : held)
-        if (b->pins[i].refs && --b->pins[i].refs == 0) (void)hipHostUnregister(reinterpret_cast<void*>(b->pins[i].lo));
-    (void)hipGetLastError();
-}
-
 int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint32_t* pool) {
     if (!b || !base || !bytes || !pool || (uintptr_t)base + bytes < (uintptr_t)base) return CYAES_EINVAL;
     std::lock_guard<std::mutex> lk(b->pmu);
@@ -1082,16 +988,18 @@ int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint
     // Pin the whole pages the range covers (the caller's buffer need not be page aligned).
     const uintptr_t lo = (uintptr_t)base & ~(uintptr_t)4095;
     const uintptr_t hi = ((uintptr_t)base + bytes + 4095) & ~(uintptr_t)4095;
-    std::vector<size_t> held;
-    int st = pin_span(b, lo, hi, &held);
+    cyaes::PinHold held;
+    int st = cyaes::pin_acquire(lo, hi, cyaes::PinMode::kShared, &held);
+    if (st == cyaes::kPinConflict) st = CYAES_EINVAL;  // part of the pages registered by another owner
     // The device view must be one contiguous range: check it at the end and at
     // every boundary between the registrations that hold the pool.
     void* dev = nullptr;
     if (st == CYAES_OK && hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) st = CYAES_EINVAL;
     if (st == CYAES_OK) {
-        std::vector<uintptr_t> probe{(uintptr_t)base + bytes - 1};
-        for (size_t i : held)
-            for (uintptr_t q : {b->pins[i].lo, b->pins[i].hi - 1, b->pins[i].hi})
+        std::vector<uintptr_t> probe{(uintptr_t)base + bytes - 1}, bounds;
+        cyaes::pin_bounds(held, &bounds);
+        for (size_t i = 0; i < bounds.size(); i += 2)
+            for (uintptr_t q : {bounds[i], bounds[i + 1] - 1, bounds[i + 1]})
                 if (q > (uintptr_t)base && q < (uintptr_t)base + bytes) probe.push_back(q);
         for (uintptr_t q : probe) {
             void* dq = nullptr;
@@ -1103,7 +1011,7 @@ int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint
         }
     }
     if (st != CYAES_OK) {
-        unpin(b, held);
+        (void)cyaes::pin_release(&held);
         (void)hipGetLastError();
         (void)hipSetDevice(dev_prev);
         return st;
@@ -1118,13 +1026,12 @@ int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint
 
 int cyaes_batcher_unregister_pool(cyaes_batcher* b, uint32_t pool) {
     if (!b || pool >= (uint32_t)kMaxPools) return CYAES_EINVAL;
-    std::vector<size_t> held;  // its pins' refs stay taken until the requests below are done
+    cyaes::PinHold held;  // its references stay taken until the requests below are done
     {
         std::lock_guard<std::mutex> lk(b->pmu);
         if (!b->pools[pool].live) return CYAES_EINVAL;
         b->pools[pool].live = false;
-        held = std::move(b->pool_pins[pool]);
-        b->pool_pins[pool].clear();
+        std::swap(held, b->pool_pins[pool]);
         b->pools_version.fetch_add(1, std::memory_order_release);
     }
     // Requests enqueued before the removal may still read or write the pool.
@@ -1134,9 +1041,9 @@ int cyaes_batcher_unregister_pool(cyaes_batcher* b, uint32_t pool) {
     int dev_prev = 0;
     (void)hipGetDevice(&dev_prev);
     (void)hipSetDevice(b->cfg.device);
-    unpin(b, held);  // pages another live pool still uses stay pinned
+    const int st = cyaes::pin_release(&held);  // pages another live pool still uses stay registered
     (void)hipSetDevice(dev_prev);
-    return CYAES_OK;
+    return st;
 }
 
 int cyaes_batcher_submit_many(cyaes_batcher* b, const cyaes_batch_req* reqs, uint32_t n, int* status) {

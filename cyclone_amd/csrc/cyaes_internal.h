@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 struct cyaes_gpu;  // include/cyaes.h
 
 namespace cyaes {
@@ -102,17 +104,16 @@ struct EncArgs {
                              // (cyaes_gpu_encrypt_strided; offsets / nbytes are not read)
 };
 
-// Per-launch decrypt scratch (DecArgs.work): words kWorkLeadOff + workgroup
-// are the progress-feedback leader words, words kWorkCtrOff + 64 * x the
-// ticket counters of the dynamic pools, one per XCD (a 256-B line each).  Per
+// Per-launch decrypt scratch (DecArgs.work): words kWorkCtrOff + 64 * x are
+// the ticket counters of the dynamic pools, one per XCD (a 256-B line each),
+// and words kWorkLeadOff + workgroup, after all of them, the progress-feedback
+// leader words, so no grid size can make the two overlap.  Per
 // launch, so concurrent decrypts on different streams never share them
 // (VERDICT r03, weak 7).
-constexpr uint32_t kWorkLeadOff = 64;
-constexpr uint32_t kWorkCtrOff = 512;
+constexpr uint32_t kWorkCtrOff = 0;
 constexpr uint32_t kXcds = 8;  // MI355X; on a chip with fewer, the spare pools are simply stolen from
-constexpr uint32_t dec_work_words(uint32_t grid) {
-    return kWorkCtrOff + 64 * kXcds > kWorkLeadOff + grid ? kWorkCtrOff + 64 * kXcds : kWorkLeadOff + grid;
-}
+constexpr uint32_t kWorkLeadOff = kWorkCtrOff + 64 * kXcds;
+constexpr uint32_t dec_work_words(uint32_t grid) { return kWorkLeadOff + grid; }
 
 struct DecArgs {
     const uint8_t* in;
@@ -214,5 +215,25 @@ bool ragged_encrypt_is_quad(const cyaes_gpu* ctx, uint64_t n);
 int ragged_batch(cyaes_gpu* ctx, bool decrypt, const uint32_t* d_table, uint32_t table_keys, const uint8_t* in,
                  uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes, uint64_t npayloads,
                  const uint32_t* key_idx, hipStream_t stream);
+
+// Host-memory registrations (cyaes_pins.cpp): every hipHostRegister the
+// library makes, in one process-wide registry.
+constexpr uintptr_t kPinPage = 4096;
+constexpr int kPinConflict = 1;  // internal: pages another owner (or a host batch) holds
+enum class PinMode {
+    kShared,     // a batcher pool: page-aligned span, shared with other pools' registrations by reference count
+    kExclusive,  // a host batch's buffer: the exact byte range, on pages no other registration touches
+};
+struct PinHold {
+    std::vector<uintptr_t> regs;  // registry entries holding the range, one reference each
+    bool foreign = false;         // inside one registration of another owner: used as it is, nothing held
+};
+// CYAES_OK (held or foreign), kPinConflict, or an error; on failure nothing is held.
+int pin_acquire(uintptr_t lo, uintptr_t hi, PinMode mode, PinHold* h);
+// Drops the references; unregisters what no one holds any more.  Returns
+// CYAES_EDEVICE if an unregister failed or left the runtime answering for the range.
+int pin_release(PinHold* h);
+// [lo, hi) of each registration held (the batcher's device-view checks).
+void pin_bounds(const PinHold& h, std::vector<uintptr_t>* out);
 
 }  // namespace cyaes

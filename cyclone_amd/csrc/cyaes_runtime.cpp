@@ -41,12 +41,23 @@ struct cyaes_gpu {
     struct ScratchBlock {
         void* p;
         uint64_t bytes;
-        hipEvent_t done;  // recorded on the last user's stream behind its kernels
-        bool in_use;      // held by a call that is still enqueuing
-        bool pending;     // `done` recorded and not yet seen complete
+        hipEvent_t done;     // recorded on the last user's stream behind its kernels
+        hipStream_t stream;  // that stream
+        bool in_use;         // held by a call that is still enqueuing
+        bool pending;        // `done` recorded and not yet seen complete
     };
     std::mutex scratch_mu;
     std::vector<ScratchBlock> scratch;
+    uint64_t scratch_bytes = 0;  // cached in `scratch`
+    // Key table (d_keys) users: per stream that ran a batch reading it, an event
+    // recorded behind that batch's kernels, so a write of the table waits for
+    // exactly those streams, not for the device.
+    std::mutex key_mu;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> key_uses;
+    hipStream_t key_stream = nullptr;     // private, non-blocking: the table's host-side writes and reads
+    hipEvent_t keys_written = nullptr;    // behind cyaes_gpu_set_keys_device's expansion on the caller's stream
+    bool keys_written_pending = false;
+    std::vector<uint32_t*> retired_keys;  // tables outgrown while batches may still read them; freed at destroy
 };
 
 namespace {
@@ -95,6 +106,21 @@ int make_keysel(const cyaes_gpu* ctx, uint64_t npayloads, const uint32_t* key_id
     ks->ppk = key_idx ? make_fastdiv(0) : make_fastdiv(ppk);
     ks->nkeys = nkeys;
     return CYAES_OK;
+}
+
+// A batch that read the context's key table was launched on `stream`.
+bool reads_ctx_keys(const cyaes_gpu* ctx, const uint32_t* table) {
+    return ctx->d_keys && table >= ctx->d_keys && table < ctx->d_keys + (uint64_t)ctx->key_cap * kSchedWords;
+}
+int note_key_use(cyaes_gpu* ctx, const uint32_t* table, hipStream_t stream) {
+    if (!reads_ctx_keys(ctx, table)) return CYAES_OK;
+    std::lock_guard<std::mutex> lk(ctx->key_mu);
+    for (auto& u : ctx->key_uses)
+        if (u.first == stream) return map_err(hipEventRecord(u.second, stream));
+    hipEvent_t ev = nullptr;
+    CY_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    ctx->key_uses.push_back({stream, ev});
+    return map_err(hipEventRecord(ev, stream));
 }
 
 constexpr uint64_t kRunMax = 8;               // payloads per encrypt run
@@ -157,7 +183,8 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
         // Latency-bound batch (fewer chains than lanes to fill the chip four
         // times over), or a ragged one: four lanes per chain (k_encrypt_quad).
         const Shape sh = wave_shape(ctx, (4 * npayloads + 63) / 64, kEncThreads);
-        return map_err(launch_encrypt_quad(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
+        CY_TRY(launch_encrypt_quad(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
+        return note_key_use(ctx, a.keys.table, stream);
     }
     // Runs (k_encrypt RUNS): a uniform batch of short payloads with more
     // payloads than the chip has lanes gives each lane R consecutive payloads
@@ -199,7 +226,8 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     // schedule once, before its loop); more workgroups than CUs queue.
     const uint64_t sess_grid = (waves * 64 + sh.threads - 1) / sh.threads;
     if (sess && sess_grid > (uint64_t)INT32_MAX) return CYAES_EINVAL;
-    return map_err(launch_encrypt(a, sess ? (int)sess_grid : std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
+    CY_TRY(launch_encrypt(a, sess ? (int)sess_grid : std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
+    return note_key_use(ctx, a.keys.table, stream);
 }
 
 // Per-call device scratch (the decrypt's work words and range-boundary
@@ -216,7 +244,8 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
 // of this library launched since a device-wide synchronisation: the pool's
 // deferred release is the suspect, so the library no longer uses the
 // stream-ordered allocator)
-constexpr size_t kScratchMaxBlocks = 64;  // beyond this, wait for a pending block instead of allocating
+constexpr size_t kScratchMaxBlocks = 64;             // beyond this, reuse a pending block behind its event
+constexpr uint64_t kScratchCacheBytes = 256ull << 20;  // above this, completed blocks are freed, largest first
 
 struct StreamScratch {
     void* p = nullptr;
@@ -226,14 +255,19 @@ struct StreamScratch {
     int get(cyaes_gpu* c, uint64_t bytes, hipStream_t stream) {
         std::lock_guard<std::mutex> lk(c->scratch_mu);
         auto& v = c->scratch;
-        size_t best = v.size(), oldest = v.size();
+        // Preference: a completed block, or one whose last user was this very
+        // stream (stream order already puts this call behind it), smallest
+        // first; else, at the block limit, a pending block of another stream,
+        // which this stream then waits for on the device (never
+        // block the host under the mutex).
+        size_t best = v.size(), other = v.size();
         for (size_t i = 0; i < v.size(); i++) {
             auto& b = v[i];
-            if (b.in_use || b.bytes < bytes) continue;
-            if (b.pending) {
+            if (!b.p || b.in_use || b.bytes < bytes) continue;
+            if (b.pending && b.stream != stream) {
                 const hipError_t q = hipEventQuery(b.done);
                 if (q == hipErrorNotReady) {
-                    if (oldest == v.size()) oldest = i;
+                    if (other == v.size() || b.bytes < v[other].bytes) other = i;
                     continue;
                 }
                 if (q != hipSuccess) return map_err(q);
@@ -241,14 +275,15 @@ struct StreamScratch {
             }
             if (best == v.size() || b.bytes < v[best].bytes) best = i;
         }
-        if (best == v.size() && v.size() >= kScratchMaxBlocks && oldest != v.size()) {
-            CY_TRY(hipEventSynchronize(v[oldest].done));
-            v[oldest].pending = false;
-            best = oldest;
+        const size_t live = (size_t)std::count_if(v.begin(), v.end(), [](const auto& b) { return b.p != nullptr; });
+        if (best == v.size() && live >= kScratchMaxBlocks && other != v.size()) {
+            CY_TRY(hipStreamWaitEvent(stream, v[other].done, 0));
+            best = other;
         }
         if (best == v.size()) {
             uint64_t cap = 4096;
             while (cap < bytes) cap *= 2;
+            trim(c, cap);
             void* mem = nullptr;
             CY_TRY(hipMalloc(&mem, cap));
             hipEvent_t ev = nullptr;
@@ -257,8 +292,12 @@ struct StreamScratch {
                 (void)hipFree(mem);
                 return map_err(e);
             }
-            v.push_back({mem, cap, ev, false, false});
-            best = v.size() - 1;
+            size_t slot = 0;  // a slot trim() emptied, else a new one
+            while (slot < v.size() && v[slot].p) slot++;
+            if (slot == v.size()) v.push_back({});
+            v[slot] = {mem, cap, ev, stream, false, false};
+            c->scratch_bytes += cap;
+            best = slot;
         }
         v[best].in_use = true;
         p = v[best].p;
@@ -267,6 +306,28 @@ struct StreamScratch {
         s = stream;
         return CYAES_OK;
     }
+    // Before caching `adding` more bytes: frees completed blocks, largest
+    // first, while the cache would exceed kScratchCacheBytes (a large call's
+    // block is not kept for the context's life).  hipFree may wait
+    // for the device, so this runs only when a block is about to be allocated
+    // anyway and the cache is over its cap.
+    static void trim(cyaes_gpu* c, uint64_t adding) {
+        auto& v = c->scratch;
+        while (c->scratch_bytes + adding > kScratchCacheBytes) {
+            size_t big = v.size();
+            for (size_t i = 0; i < v.size(); i++) {
+                const auto& b = v[i];
+                if (!b.p || b.in_use || (b.pending && hipEventQuery(b.done) != hipSuccess)) continue;
+                if (big == v.size() || b.bytes > v[big].bytes) big = i;
+            }
+            (void)hipGetLastError();
+            if (big == v.size()) return;
+            (void)hipFree(v[big].p);
+            (void)hipEventDestroy(v[big].done);
+            c->scratch_bytes -= v[big].bytes;
+            v[big] = {};  // an empty slot: the indices held by calls in flight stay valid
+        }
+    }
     ~StreamScratch() {
         if (!p) return;
         std::lock_guard<std::mutex> lk(ctx->scratch_mu);
@@ -274,6 +335,7 @@ struct StreamScratch {
         // after the kernels queued on s; if the record fails, the block stays
         // out of use until the context is destroyed (its synchronisation)
         b.pending = hipEventRecord(b.done, s) == hipSuccess;
+        b.stream = s;
         b.in_use = !b.pending;
     }
 };
@@ -383,7 +445,8 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     // progress words are reset by their workgroups.  A small static batch (the
     // drop-in's packet) launches the kernel alone, as before.
     if (a.dyn || a.boundary) CY_TRY(launch_dec_prepass(a, ww, stream));
-    return map_err(launch_decrypt_flat(a, grid, stream));
+    CY_TRY(launch_decrypt_flat(a, grid, stream));
+    return note_key_use(ctx, a.keys.table, stream);
 }
 
 int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
@@ -434,7 +497,8 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     if (st) return st;
     a.work = static_cast<uint32_t*>(work.p);
     if (a.dyn) CY_TRY(launch_dec_prepass(a, ww, stream));
-    return map_err(launch_decrypt_ragged(a, grid, sh.threads, stream));
+    CY_TRY(launch_decrypt_ragged(a, grid, sh.threads, stream));
+    return note_key_use(ctx, a.keys.table, stream);
 }
 
 bool aligned4(const void* p) { return ((uintptr_t)p & 3u) == 0; }
@@ -527,6 +591,8 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_status), 16);
     if (e == hipSuccess) e = hipMemset(ctx->d_status, 0, 16);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_digest), 16);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->key_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->keys_written, hipEventDisableTiming);
     if (e != hipSuccess) {
         cyaes_gpu_destroy(ctx);
         return map_err(e);
@@ -546,11 +612,16 @@ int cyaes_gpu_destroy(cyaes_gpu* ctx) {
     (void)hipFree(ctx->d_keys);
     (void)hipFree(ctx->d_status);
     (void)hipFree(ctx->d_digest);
+    for (uint32_t* k : ctx->retired_keys) (void)hipFree(k);
     destroy_pipe(ctx->pipe);
     for (auto& b : ctx->scratch) {  // (every batch has completed: the synchronisation above)
+        if (!b.p) continue;
         (void)hipFree(b.p);
         (void)hipEventDestroy(b.done);
     }
+    for (auto& u : ctx->key_uses) (void)hipEventDestroy(u.second);
+    if (ctx->keys_written) (void)hipEventDestroy(ctx->keys_written);
+    if (ctx->key_stream) (void)hipStreamDestroy(ctx->key_stream);
     delete ctx;
     return map_err(e);
 }
@@ -559,32 +630,79 @@ int cyaes_gpu_device(const cyaes_gpu* ctx) { return ctx ? ctx->device : -1; }
 int cyaes_gpu_num_cus(const cyaes_gpu* ctx) { return ctx ? ctx->num_cus : 0; }
 uint32_t cyaes_gpu_nkeys(const cyaes_gpu* ctx) { return ctx ? ctx->nkeys : 0; }
 
-static int reserve_keys(cyaes_gpu* ctx, uint32_t nkeys) {
+// The key table's writers wait only for the streams that read it: each
+// stream's last batch under this context's table (note_key_use), and an
+// expansion cyaes_gpu_set_keys_device queued on a caller's stream.
+static int wait_key_readers(cyaes_gpu* ctx) {
+    std::lock_guard<std::mutex> lk(ctx->key_mu);
+    for (auto& u : ctx->key_uses) CY_TRY(hipEventSynchronize(u.second));
+    return CYAES_OK;
+}
+static int wait_key_writes(cyaes_gpu* ctx) {
+    if (ctx->keys_written_pending) {
+        CY_TRY(hipEventSynchronize(ctx->keys_written));
+        ctx->keys_written_pending = false;
+    }
+    return CYAES_OK;
+}
+
+// Grows the table to hold nkeys rows.  The outgrown table is kept until the
+// context is destroyed (batches queued before may still read it; hipFree
+// would wait for the whole device), so a grown table needs no wait at all.
+// *grown tells whether the table is new (nothing reads it yet).
+static int reserve_keys(cyaes_gpu* ctx, uint32_t nkeys, uint32_t keep_rows, bool* grown) {
+    *grown = false;
     if (ctx->key_cap >= nkeys) return CYAES_OK;
-    if (ctx->d_keys) CY_TRY(hipFree(ctx->d_keys));  // hipFree waits for pending work
-    ctx->d_keys = nullptr;
-    ctx->key_cap = 0;
-    CY_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->d_keys), (uint64_t)nkeys * kSchedWords * 4));
-    ctx->key_cap = nkeys;
+    const uint32_t cap = std::max(nkeys, ctx->key_cap * 2);
+    uint32_t* t = nullptr;
+    CY_TRY(hipMalloc(reinterpret_cast<void**>(&t), (uint64_t)cap * kSchedWords * 4));
+    if (keep_rows) {
+        int st = wait_key_writes(ctx);
+        hipError_t e = st ? hipErrorUnknown
+                          : hipMemcpyAsync(t, ctx->d_keys, (uint64_t)keep_rows * kSchedWords * 4,
+                                           hipMemcpyDeviceToDevice, ctx->key_stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->key_stream);
+        if (e != hipSuccess) {
+            (void)hipFree(t);
+            return st ? st : map_err(e);
+        }
+    }
+    if (ctx->d_keys) ctx->retired_keys.push_back(ctx->d_keys);
+    ctx->d_keys = t;
+    ctx->key_cap = cap;
+    *grown = true;
+    return CYAES_OK;
+}
+
+// Writes rows [first, first + n) from host schedules: in place only after the
+// streams that read the table are done with it.
+static int write_key_rows(cyaes_gpu* ctx, uint32_t first, const uint32_t* host, uint32_t n, bool fresh_table) {
+    if (!fresh_table) {
+        int st = wait_key_readers(ctx);
+        if (st) return st;
+    }
+    int st = wait_key_writes(ctx);
+    if (st) return st;
+    CY_TRY(hipMemcpyAsync(ctx->d_keys + (uint64_t)first * kSchedWords, host, (uint64_t)n * kSchedWords * 4,
+                          hipMemcpyHostToDevice, ctx->key_stream));
+    CY_TRY(hipStreamSynchronize(ctx->key_stream));
     return CYAES_OK;
 }
 
 int cyaes_gpu_set_keys(cyaes_gpu* ctx, const uint8_t* keys, uint32_t nkeys) {
     if (!ctx || !keys || nkeys == 0) return CYAES_EINVAL;
     DeviceGuard g(ctx->device);
-    int st = reserve_keys(ctx, nkeys);
-    if (st) return st;
-    uint32_t* host = (uint32_t*)malloc((size_t)nkeys * kSchedWords * 4);
-    if (!host) return CYAES_ENOMEM;
+    std::vector<uint32_t> host((size_t)nkeys * kSchedWords);
     for (uint32_t i = 0; i < nkeys; i++) {
         cyaes_key k;
         expand_key(keys + 16ull * i, &k);
-        to_device_schedule(k, host + (size_t)i * kSchedWords);
+        to_device_schedule(k, host.data() + (size_t)i * kSchedWords);
     }
-    hipError_t e = hipDeviceSynchronize();  // no batch may still read the old table
-    if (e == hipSuccess) e = hipMemcpy(ctx->d_keys, host, (size_t)nkeys * kSchedWords * 4, hipMemcpyHostToDevice);
-    free(host);
-    if (e != hipSuccess) return map_err(e);
+    bool grown = false;
+    int st = reserve_keys(ctx, nkeys, 0, &grown);
+    if (st) return st;
+    st = write_key_rows(ctx, 0, host.data(), nkeys, grown);
+    if (st) return st;
     ctx->nkeys = nkeys;
     return CYAES_OK;
 }
@@ -599,23 +717,12 @@ int cyaes_gpu_update_keys(cyaes_gpu* ctx, uint32_t first, const uint8_t* keys, u
         expand_key(keys + 16ull * i, &k);
         to_device_schedule(k, host.data() + (size_t)i * kSchedWords);
     }
-    CY_TRY(hipDeviceSynchronize());  // no batch may still read the rows being replaced
-    if (total > ctx->key_cap) {      // grow, keeping rows [0, first)
-        const uint32_t cap = std::max(total, ctx->key_cap * 2);
-        uint32_t* grown = nullptr;
-        CY_TRY(hipMalloc(reinterpret_cast<void**>(&grown), (uint64_t)cap * kSchedWords * 4));
-        hipError_t e = hipSuccess;
-        if (first) e = hipMemcpy(grown, ctx->d_keys, (uint64_t)first * kSchedWords * 4, hipMemcpyDeviceToDevice);
-        if (e != hipSuccess) {
-            (void)hipFree(grown);
-            return map_err(e);
-        }
-        (void)hipFree(ctx->d_keys);
-        ctx->d_keys = grown;
-        ctx->key_cap = cap;
-    }
-    CY_TRY(hipMemcpy(ctx->d_keys + (uint64_t)first * kSchedWords, host.data(), host.size() * 4,
-                     hipMemcpyHostToDevice));
+    bool grown = false;  // grow, keeping rows [0, first)
+    int st = reserve_keys(ctx, total, first, &grown);
+    if (st) return st;
+    // Appended rows only (first == nkeys) are rows no queued batch can read either.
+    st = write_key_rows(ctx, first, host.data(), n, grown || first == ctx->nkeys);
+    if (st) return st;
     ctx->nkeys = total;
     return CYAES_OK;
 }
@@ -623,10 +730,19 @@ int cyaes_gpu_update_keys(cyaes_gpu* ctx, uint32_t first, const uint8_t* keys, u
 int cyaes_gpu_set_keys_device(cyaes_gpu* ctx, const uint8_t* d_keys, uint32_t nkeys, void* stream) {
     if (!ctx || !d_keys || nkeys == 0) return CYAES_EINVAL;
     DeviceGuard g(ctx->device);
-    int st = reserve_keys(ctx, nkeys);
+    bool grown = false;
+    int st = reserve_keys(ctx, nkeys, 0, &grown);
     if (st) return st;
+    hipStream_t s = (hipStream_t)stream;
+    if (!grown) {  // the expansion waits (on the device) for the streams still reading the table
+        std::lock_guard<std::mutex> lk(ctx->key_mu);
+        for (auto& u : ctx->key_uses)
+            if (u.first != s) CY_TRY(hipStreamWaitEvent(s, u.second, 0));
+    }
     const uint8_t* d_sbox = reinterpret_cast<const uint8_t*>(ctx->d_tables) + kSboxOff;
-    CY_TRY(launch_key_expand(d_keys, nkeys, d_sbox, ctx->d_keys, (hipStream_t)stream));
+    CY_TRY(launch_key_expand(d_keys, nkeys, d_sbox, ctx->d_keys, s));
+    CY_TRY(hipEventRecord(ctx->keys_written, s));
+    ctx->keys_written_pending = true;
     ctx->nkeys = nkeys;
     return CYAES_OK;
 }
@@ -636,8 +752,11 @@ int cyaes_gpu_get_key(cyaes_gpu* ctx, uint32_t index, cyaes_key* out) {
     if (index >= ctx->nkeys) return CYAES_ERANGE;
     DeviceGuard g(ctx->device);
     uint32_t w[kSchedWords];
-    CY_TRY(hipDeviceSynchronize());
-    CY_TRY(hipMemcpy(w, ctx->d_keys + (uint64_t)index * kSchedWords, sizeof(w), hipMemcpyDeviceToHost));
+    int st = wait_key_writes(ctx);
+    if (st) return st;
+    CY_TRY(hipMemcpyAsync(w, ctx->d_keys + (uint64_t)index * kSchedWords, sizeof(w), hipMemcpyDeviceToHost,
+                          ctx->key_stream));
+    CY_TRY(hipStreamSynchronize(ctx->key_stream));
     from_device_schedule(w, out);
     return CYAES_OK;
 }
@@ -1105,7 +1224,12 @@ struct HostPipe {
     uint8_t* d_in[kSlots] = {};
     uint8_t* d_out[kSlots] = {};
     uint64_t cap = 0;
+    // Pinned staging for caller ranges that are bounced instead of registered
+    // (HostPin): created on first use, kBounceChunk bytes per slot.
+    uint8_t* h_stage[kSlots] = {};
+    uint64_t stage_cap = 0;
 };
+constexpr uint64_t kBounceChunk = 32ull << 20;
 
 static void destroy_pipe(HostPipe* p) {
     if (!p) return;
@@ -1116,6 +1240,8 @@ static void destroy_pipe(HostPipe* p) {
         if (p->ev_comp[i]) (void)hipEventDestroy(p->ev_comp[i]);
         if (p->ev_down[i]) (void)hipEventDestroy(p->ev_down[i]);
     }
+    for (int i = 0; i < HostPipe::kSlots; i++)
+        if (p->h_stage[i]) (void)hipHostFree(p->h_stage[i]);
     for (hipStream_t s : {p->up, p->comp, p->down})
         if (s) (void)hipStreamDestroy(s);
     delete p;
@@ -1137,7 +1263,7 @@ int pipe_ready(cyaes_gpu* ctx, uint64_t slot_bytes) {
     }
     HostPipe* p = ctx->pipe;
     if (p->cap < slot_bytes) {
-        CY_TRY(hipDeviceSynchronize());
+        for (hipStream_t s : {p->up, p->comp, p->down}) CY_TRY(hipStreamSynchronize(s));  // the slots' only users
         for (int i = 0; i < HostPipe::kSlots; i++) {
             (void)hipFree(p->d_in[i]);
             (void)hipFree(p->d_out[i]);
@@ -1153,30 +1279,40 @@ int pipe_ready(cyaes_gpu* ctx, uint64_t slot_bytes) {
     return CYAES_OK;
 }
 
-bool host_pinned(const void* ptr) {
-    hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, ptr) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
+int stage_ready(HostPipe* p, uint64_t bytes) {
+    if (p->stage_cap >= bytes) return CYAES_OK;
+    for (int i = 0; i < HostPipe::kSlots; i++) {
+        if (p->h_stage[i]) CY_TRY(hipHostFree(p->h_stage[i]));  // (the pipe's streams are idle between calls)
+        p->h_stage[i] = nullptr;
     }
-    return at.type == hipMemoryTypeHost;
+    p->stage_cap = 0;
+    for (int i = 0; i < HostPipe::kSlots; i++)
+        CY_TRY(hipHostMalloc(reinterpret_cast<void**>(&p->h_stage[i]), bytes, hipHostMallocDefault));
+    p->stage_cap = bytes;
+    return CYAES_OK;
 }
 
-// Pins a pageable host range for the duration of a call (DMA straight from
-// and to the caller's memory instead of the runtime's bounce buffers).  A
-// range that cannot be registered is left pageable; the copies still work.
+// A caller's host range for the duration of one host batch (cyaes_pins.cpp).
+// Registered as its exact bytes when no page of it is registered by anyone;
+// used as it is when it lies inside one registration of another owner
+// (hipHostMalloc, the caller's own hipHostRegister); otherwise -- pages shared
+// with another registration, such as the other buffer of this call on a
+// shared heap page -- it is not registered at all and its chunks are bounced
+// through the pipe's pinned staging slots (direct == false).  r04's two
+// illegal-address faults are the reason nothing is registered over anyone's
+// pages any more.
 struct HostPin {
-    void* ptr = nullptr;
-    explicit HostPin(const void* p, uint64_t bytes) {
-        if (host_pinned(p)) return;
-        if (hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) == hipSuccess)
-            ptr = const_cast<void*>(p);
-        else
-            (void)hipGetLastError();
+    PinHold h;
+    bool direct = false;  // DMA straight from / to the caller's memory
+    void acquire(const void* p, uint64_t bytes) {
+        // Any failure to register (a conflict, a pinning limit) bounces.
+        direct = pin_acquire((uintptr_t)p, (uintptr_t)p + bytes, PinMode::kExclusive, &h) == CYAES_OK;
     }
-    ~HostPin() {
-        if (ptr) (void)hipHostUnregister(ptr);
+    int release() {
+        direct = false;
+        return pin_release(&h);
     }
+    ~HostPin() { (void)pin_release(&h); }  // (early returns; the explicit release reports the status)
 };
 
 struct PipeDrain {
@@ -1192,31 +1328,59 @@ int host_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* h_in, uint8_t* h_out
     if (npayloads == 0 || payload_bytes == 0) return CYAES_OK;
     if (ctx->nkeys == 0) return CYAES_ERANGE;
     if (ppk && (npayloads - 1) / ppk >= ctx->nkeys) return CYAES_ERANGE;
+    if (npayloads > UINT64_MAX / payload_bytes) return CYAES_EINVAL;
     DeviceGuard g(ctx->device);
     if (!g.ok) return CYAES_EDEVICE;
     if (chunk_bytes == 0) chunk_bytes = 256ull << 20;
+    const uint64_t total = npayloads * payload_bytes;
+    const bool inplace = h_out == h_in;
+    HostPin pin_in, pin_out;
+    pin_in.acquire(h_in, total);
+    if (!inplace) pin_out.acquire(h_out, total);
+    const bool bounce_in = !pin_in.direct, bounce_out = inplace ? bounce_in : !pin_out.direct;
+    if (bounce_in || bounce_out) chunk_bytes = std::min(chunk_bytes, kBounceChunk);
     // Chunks hold whole payloads, and whole sessions when keys are per session,
     // so chunk c starts at session c0 / ppk and runs under that table slice.
     uint64_t cp = std::max<uint64_t>(1, chunk_bytes / payload_bytes);
     if (ppk) cp = std::max<uint64_t>(ppk, cp / ppk * ppk);
     cp = std::min(cp, npayloads);
-    const uint64_t total = npayloads * payload_bytes;
     int st = pipe_ready(ctx, cp * payload_bytes);
     if (st) return st;
-    HostPin pin_in(h_in, total);
-    HostPin pin_out(h_out, (h_out == h_in) ? 0 : total);
     HostPipe* p = ctx->pipe;
+    if (bounce_in || bounce_out) {
+        st = stage_ready(p, cp * payload_bytes);
+        if (st) return st;
+    }
     // Declared after the pins, so destroyed before them: on every return,
     // early ones included, the copies queued from and to the caller's pages
-    // have finished before ~HostPin unregisters those pages.
+    // (and the staging slots) have finished before the pins are released.
     PipeDrain drain{p};
-    uint64_t i = 0;
-    for (uint64_t c0 = 0; c0 < npayloads; c0 += cp, i++) {
+    // Chunk i's output, bounced: copied out of its staging slot once its download is done.
+    auto bounce_out_chunk = [&](uint64_t i) -> int {
         const int s = (int)(i % HostPipe::kSlots);
-        const uint64_t n = std::min(cp, npayloads - c0);
+        const uint64_t c0 = i * cp, n = std::min(cp, npayloads - c0);
+        CY_TRY(hipEventSynchronize(p->ev_down[s]));
+        memcpy(h_out + c0 * payload_bytes, p->h_stage[s], n * payload_bytes);
+        return CYAES_OK;
+    };
+    const uint64_t nchunks = (npayloads + cp - 1) / cp;
+    for (uint64_t i = 0; i < nchunks; i++) {
+        const int s = (int)(i % HostPipe::kSlots);
+        const uint64_t c0 = i * cp, n = std::min(cp, npayloads - c0);
         const uint64_t off = c0 * payload_bytes, bytes = n * payload_bytes;
+        if (i >= (uint64_t)HostPipe::kSlots && bounce_out) {
+            st = bounce_out_chunk(i - HostPipe::kSlots);  // frees the staging slot, too
+            if (st) return st;
+        } else if (i >= (uint64_t)HostPipe::kSlots && bounce_in) {
+            CY_TRY(hipEventSynchronize(p->ev_up[s]));  // the slot's previous upload has read it
+        }
         if (i >= (uint64_t)HostPipe::kSlots) CY_TRY(hipStreamWaitEvent(p->up, p->ev_comp[s], 0));
-        CY_TRY(hipMemcpyAsync(p->d_in[s], h_in + off, bytes, hipMemcpyHostToDevice, p->up));
+        const uint8_t* src = h_in + off;
+        if (bounce_in) {
+            memcpy(p->h_stage[s], src, bytes);
+            src = p->h_stage[s];
+        }
+        CY_TRY(hipMemcpyAsync(p->d_in[s], src, bytes, hipMemcpyHostToDevice, p->up));
         CY_TRY(hipEventRecord(p->ev_up[s], p->up));
         CY_TRY(hipStreamWaitEvent(p->comp, p->ev_up[s], 0));
         if (i >= (uint64_t)HostPipe::kSlots) CY_TRY(hipStreamWaitEvent(p->comp, p->ev_down[s], 0));
@@ -1230,11 +1394,24 @@ int host_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* h_in, uint8_t* h_out
         if (st) return st;
         CY_TRY(hipEventRecord(p->ev_comp[s], p->comp));
         CY_TRY(hipStreamWaitEvent(p->down, p->ev_comp[s], 0));
-        CY_TRY(hipMemcpyAsync(h_out + off, p->d_out[s], bytes, hipMemcpyDeviceToHost, p->down));
+        // A bounced output lands in the slot's staging buffer, which its upload
+        // has already been read from (the download waits for the kernel, which
+        // waited for the upload).
+        CY_TRY(hipMemcpyAsync(bounce_out ? p->h_stage[s] : h_out + off, p->d_out[s], bytes, hipMemcpyDeviceToHost,
+                              p->down));
         CY_TRY(hipEventRecord(p->ev_down[s], p->down));
     }
+    if (bounce_out)
+        for (uint64_t i = nchunks > (uint64_t)HostPipe::kSlots ? nchunks - HostPipe::kSlots : 0; i < nchunks; i++) {
+            st = bounce_out_chunk(i);
+            if (st) return st;
+        }
     CY_TRY(hipStreamSynchronize(p->down));
-    return CYAES_OK;  // (drain finds the streams idle)
+    for (hipStream_t s : {p->up, p->comp}) CY_TRY(hipStreamSynchronize(s));
+    // (the drain finds the streams idle)
+    const int r_out = pin_out.release();
+    const int r_in = pin_in.release();
+    return r_in ? r_in : r_out;
 }
 
 }  // namespace

@@ -198,6 +198,19 @@ int cyaes_gpu_fill_synthetic(uint8_t* d_buf, uint64_t p0, uint64_t npayloads, ui
  * Synchronous (waits on `stream`). */
 int cyaes_gpu_digest(const uint8_t* d_buf, uint64_t nbytes, uint64_t out[2], void* stream);
 
+/* ---- Diagnostics --------------------------------------------------------
+ * Host-memory registrations the library holds (cyclone_amd/csrc/cyaes_pins.cpp:
+ * the batcher's packet pools and the host batches' pageable buffers; every
+ * hipHostRegister the library makes goes through one process-wide registry).
+ * out[0] live registrations, out[1] live registered bytes, out[2] registrations
+ * made, out[3] unregistered, out[4] unregisters that failed, out[5] unregisters
+ * after which the runtime still answered for the range, out[6] requests not
+ * registered because another owner's registration (or a host batch's) held
+ * some of their pages (pools refused, host batches bounced), out[7] references
+ * held.  Out[4] and out[5] are 0 unless the runtime misbehaves; out[0] is 0
+ * whenever no pool is registered and no host batch runs. */
+int cyaes_debug_pins(uint64_t out[8]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,6 +34,11 @@ def _gpu_fault_guard(request):
     torch.cuda.synchronize()
     import cyclone_amd
     lib = cyclone_amd.load_library()
+    # Host-memory registrations: nothing the library registered outlives the
+    # test that made it, and every unregister took (cyaes_pins.cpp).
+    pins = cyclone_amd.debug_pins()
+    assert pins["live"] == 0 and pins["refs"] == 0, "library host registrations still live: %s" % pins
+    assert pins["failed_unregisters"] == 0 and pins["stale"] == 0, "host unregister failed: %s" % pins
     fn = getattr(lib, "cyaes_debug_bounds", None)
     if fn is not None:
         rec = (ctypes.c_ulonglong * 20)()

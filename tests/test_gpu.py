@@ -429,6 +429,146 @@ def test_host_batches_streamed(torch, encrypt_kernel, pinned):
     c.close()
 
 
+def _pin_delta(before):
+    after = ca.debug_pins()
+    return after, {k: after[k] - before[k] for k in after}
+
+
+def test_host_batch_buffers_sharing_a_page(torch):
+    """cyaes_gpu_{en,de}crypt_host on two pageable buffers that share a page (in
+    != out, one heap block, the second starting on the first's last page): the
+    first is registered for the call (its exact bytes), the second is not
+    registered over the page the first's registration holds but bounced through
+    the pipe's pinned staging (cyaes_pins.cpp; r04's illegal-address faults,
+    DESIGN.md §4.2).  Bit-exact both ways and in place; nothing the library
+    registered outlives a call; then a torch pageable copy above 1 MiB (the size
+    from which the runtime pins a pageable copy on the fly) from a fresh buffer
+    over the freed addresses, also bit-exact.  relay_local.cpp:188-217: socket
+    buffer -> encrypt -> send."""
+    n, pb = 1500, 1472  # 2.2 MB per buffer
+    total = n * pb
+    c = ca.GpuContext(0)
+    c.set_keys(K0)
+    pt = oracle.synthetic(3, n, pb)
+    want = oracle.batch(False, [K0], 0, pt, pb, nthreads=16)
+    arena = np.zeros(2 * total + 4 * 4096, dtype=np.uint8)  # pageable
+    base = arena.ctypes.data
+    a_off = (-base) % 4096 + 16
+    b_off = a_off + total + 48
+    assert (base + a_off + total - 1) // 4096 == (base + b_off) // 4096  # one shared page
+    h_a, h_b = arena[a_off:a_off + total], arena[b_off:b_off + total]
+    h_a[:] = pt
+    for chunk in (0, 5 * 4096 * 1472 // 4096):  # one chunk; several (the 3-slot staging ring wraps)
+        h_b[:] = 0
+        before = ca.debug_pins()
+        c.encrypt_host(h_a.ctypes.data, h_b.ctypes.data, n, pb, chunk_bytes=chunk)
+        assert np.array_equal(h_b, want)
+        after, d = _pin_delta(before)
+        assert after["live"] == 0 and after["refs"] == 0
+        assert d["registered"] == 1 and d["unregistered"] == 1 and d["conflicts"] == 1  # in registered, out bounced
+        assert after["failed_unregisters"] == 0 and after["stale"] == 0
+        h_a[:] = 0
+        before = ca.debug_pins()
+        c.decrypt_host(h_b.ctypes.data, h_a.ctypes.data, n, pb, chunk_bytes=chunk)  # the other way round
+        assert np.array_equal(h_a, pt)
+        after, d = _pin_delta(before)
+        assert after["live"] == 0 and d["registered"] == 1 and d["conflicts"] == 1
+    c.encrypt_host(h_a.ctypes.data, h_a.ctypes.data, n, pb, chunk_bytes=1 << 20)  # in place, registered
+    assert np.array_equal(h_a, want)
+    assert ca.debug_pins()["live"] == 0
+    del h_a, h_b
+    arena = None
+    fresh = np.random.default_rng(5).integers(0, 256, 2 * total + 4 * 4096, dtype=np.uint8)
+    d_fresh = torch.from_numpy(fresh).to("cuda")
+    torch.cuda.synchronize()
+    assert np.array_equal(d_fresh.cpu().numpy(), fresh)
+    c.close()
+
+
+def test_host_batch_in_foreign_registrations(torch):
+    """Host batches over memory someone else registered: a buffer inside one
+    foreign registration (torch pinned memory, hipHostMalloc) is used as it is,
+    nothing registered; a pageable buffer part of which the caller registered
+    itself (torch's cudaHostRegister over its middle pages) is bounced, never
+    registered over that registration, which stays intact (its own unregister
+    succeeds).  Bit-exact."""
+    n, pb = 700, 1472
+    total = n * pb
+    c = ca.GpuContext(0)
+    c.set_keys(K0)
+    pt = oracle.synthetic(4, n, pb)
+    want = oracle.batch(False, [K0], 0, pt, pb, nthreads=16)
+    h_pin = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    h_pin.copy_(torch.from_numpy(pt))
+    before = ca.debug_pins()
+    c.encrypt_host(h_pin, h_pin, n, pb)
+    assert np.array_equal(h_pin.numpy(), want)
+    after, d = _pin_delta(before)
+    assert d["registered"] == 0 and d["conflicts"] == 0 and after["live"] == 0
+    cudart = torch.cuda.cudart()
+    if not hasattr(cudart, "cudaHostRegister"):
+        pytest.skip("torch.cuda.cudart() has no cudaHostRegister")
+    arena = np.zeros(total + 4 * 4096, dtype=np.uint8)
+    off = (-arena.ctypes.data) % 4096 + 64
+    buf = arena[off:off + total]
+    buf[:] = pt
+    lo = arena.ctypes.data + off - 64 + 2 * 4096  # pages 2..4 of the buffer, registered by "the caller"
+    assert int(cudart.cudaHostRegister(lo, 3 * 4096, 0)) == 0
+    try:
+        before = ca.debug_pins()
+        c.encrypt_host(buf.ctypes.data, buf.ctypes.data, n, pb, chunk_bytes=256 * 1472)
+        assert np.array_equal(buf, want)
+        after, d = _pin_delta(before)
+        assert d["registered"] == 0 and d["conflicts"] == 1 and after["live"] == 0
+        c.decrypt_host(buf.ctypes.data, buf.ctypes.data, n, pb)
+        assert np.array_equal(buf, pt)
+    finally:
+        assert int(cudart.cudaHostUnregister(lo)) == 0
+    c.close()
+
+
+def test_set_keys_waits_only_for_its_own_streams(torch):
+    """cyaes_gpu_set_keys waits for the streams that read its own context's key
+    table, not for the device: while a long decrypt of
+    context A runs on a stream, B.set_keys (a new session's context,
+    relay_server.cpp:224,229) returns before that decrypt ends; A.update_keys,
+    whose table the decrypt reads, returns only after it.  Both bit-exact."""
+    n, pb = 65536, 65536  # 4 GiB; three decrypts queued: ~8 ms on the GPU
+    a, b = ca.GpuContext(0), ca.GpuContext(0)
+    a.set_keys(K0)
+    ct = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
+    pt = torch.empty_like(ct)
+    a.fill_synthetic(ct, 0, n, pb, oracle.PLAINTEXT_SEED)
+    want = a.digest(ct, n * pb)
+    a.encrypt_uniform(ct, ct, n, pb)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    end = torch.cuda.Event()
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            a.decrypt_uniform(ct, pt, n, pb, stream=s.cuda_stream)
+        end.record(s)
+    keys_b = [oracle.session_key(i) for i in range(5)]
+    b.set_keys(b"".join(keys_b))
+    b_returned_early = not end.query()
+    a.update_keys(0, K0)  # the running decrypts read this row
+    a_waited = end.query()
+    torch.cuda.synchronize()
+    a.update_keys(1, oracle.session_key(9))  # appended (the table grows; the old one is kept until close)
+    assert a.get_key(0).words() == ca.key_expand(K0).words()
+    assert b_returned_early, "set_keys on another context waited for this context's decrypt"
+    assert a_waited, "update_keys returned while a batch still read the rows it replaced"
+    assert a.digest(pt, n * pb) == want
+    small = oracle.synthetic(6, 64, 1024)
+    d_in = torch.from_numpy(small.copy()).to("cuda")
+    d_out = torch.empty_like(d_in)
+    b.encrypt_uniform(d_in, d_out, 64, 1024, payloads_per_key=16)
+    assert np.array_equal(host(d_out), oracle.batch(False, keys_b, 16, small, 1024))
+    assert a.check() == ca.CYAES_OK
+    a.close()
+    b.close()
+
+
 def test_host_batch_single_key_large(torch, ctx):
     """One key, 64 KiB payloads, 4 chunks of 4 MiB."""
     n, pb = 256, 65536
