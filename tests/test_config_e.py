@@ -123,6 +123,40 @@ def test_bench_gpus_two_launches_its_own_ranks():
 
 
 @pytest.mark.gpu
+def test_bench_gpus_eight_launches_its_own_ranks():
+    """The driver's 8-GPU invocation, `python bench.py --gpus 8` with no
+    wrapper, rehearsed on the box's one device: bench.py
+    launches 8 ranks itself, exactly one JSON line comes back, with an 8-rank
+    process group, all 8 ranks reporting, every rank's pass verified against its
+    committed OpenSSL digest and rank 0's CPU baseline.  On a real 8-GPU node
+    the line differs only in dist.backend ("nccl") and dist.distinct_devices
+    (8).  Key hand-off it models: relay_server.cpp:218-240."""
+    env = dict(os.environ, CYAES_BENCH_SAME_DEVICE="1", CYAES_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--config", "E", "--e-pass-payloads",
+           "4096", "--e-passes", "8", "--steps", "2", "--warmup", "1", "--packet-configs", "none", "--no-clock",
+           "--relay-stream", "0", "--cpu-sample", "256", "--traffic", "none"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["parity"] == "bit-exact" and out["launcher"]["nproc_per_node"] == 8
+    assert out["config"]["passes"] == 8 and out["config"]["passes_per_gpu"] == 1
+    d = out["dist"]
+    assert d["backend"] == "gloo" and d["world_size"] == 8 and d["ranks_reporting"] == 8
+    assert d["distinct_devices"] == 1 and d["same_keys_all_ranks"] is True
+    shards = sorted(out["shards"], key=lambda s: s["rank"])
+    assert [s["rank"] for s in shards] == list(range(8))
+    assert [s["passes"] for s in shards] == [[r] for r in range(8)]
+    assert [s["golden_verified"] for s in shards] == [[r] for r in range(8)]
+    assert out["value"] > 0 and out["scaling"] == "strong"  # config E: the 32-pass job is fixed, split over the ranks
+    c = out["cpu_baseline"]
+    assert c and c["value"] > 0 and c["matches_gpu"] is True
+
+
+@pytest.mark.gpu
 def test_two_rank_session_keys_bit_exact():
     """bench.py --config D on 2 ranks (per-session keys): rank 0 broadcasts the
     session keys, each rank expands the sessions of its payload range
