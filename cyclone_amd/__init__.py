@@ -93,6 +93,8 @@ _SIGS = {
     "cyaes_gpu_cbc_encrypt_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "cyaes_gpu_cbc_decrypt_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "cyaes_debug_pins": (ctypes.c_int, [_u64p]),
+    "cyaes_gpu_duplex_uniform": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                                _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     # include/cyaes_relay.h
     "cyaes_relay_round16": (ctypes.c_uint32, [ctypes.c_uint32]),
     "cyaes_relay_packet_bytes": (ctypes.c_uint32, [ctypes.c_uint32]),
@@ -351,6 +353,13 @@ class GpuContext:
         _check(self._lib.cyaes_gpu_decrypt_uniform(self._h, _p(d_in), _p(d_out), npayloads, payload_bytes,
                                                    _p(key_idx), payloads_per_key, _p(iv_in), _p(iv_out),
                                                    _p(stream)), "decrypt_uniform")
+
+    def duplex_uniform(self, enc_in, enc_out, enc_npayloads, enc_payload_bytes, dec_in, dec_out, dec_npayloads,
+                       dec_payload_bytes, enc_key=0, dec_key=0, stream=None):
+        """Encrypt one uniform batch and decrypt another in one launch (cyaes_gpu_duplex_uniform)."""
+        _check(self._lib.cyaes_gpu_duplex_uniform(self._h, _p(enc_in), _p(enc_out), enc_npayloads, enc_payload_bytes,
+                                                  enc_key, _p(dec_in), _p(dec_out), dec_npayloads, dec_payload_bytes,
+                                                  dec_key, _p(stream)), "duplex_uniform")
 
     def encrypt_ragged(self, d_in, d_out, offsets, nbytes, npayloads, key_idx=None, payloads_per_key=0,
                        iv_in=None, iv_out=None, stream=None):

@@ -66,6 +66,10 @@ constexpr uint32_t kDecDynPct = 25;
 constexpr uint64_t kDecShortSteps = 256;  // steps per wave at most for the short-launch progress divisor
 constexpr uint32_t kDecRangeSteps = 4;
 constexpr uint32_t kDecGroupsPerWave = 8;
+// The duplex launch's decrypt: its workgroups arrive from their encrypt walks
+// at different times (the encrypt's tail), so a share of the work is always
+// in the dynamic pool.
+constexpr uint32_t kDuplexDynPct = 25;
 
 struct Fastdiv {  // Lemire: q = mulhi64(M, n) exact for all 32-bit n, d >= 2
     uint64_t M;
@@ -149,12 +153,21 @@ struct DecArgs {
     uint64_t off0, stride;    // flat kernel, stride != 0: payload p at byte off0 + p * stride (4-B aligned), else contiguous
 };
 
+// The duplex launch (cyaes_duplex_kernels.hip): one grid encrypts batch e,
+// then, workgroup by workgroup, decrypts batch d (unkeyed halves, no IV arrays,
+// uniform contiguous batches; d.dyn on).
+struct DuplexArgs {
+    EncArgs e;
+    DecArgs d;
+};
+
 // Launchers (cyaes_*kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t stream);
 // Four lanes per chain (latency-bound batches; threads a multiple of 64).
 hipError_t launch_encrypt_quad(const EncArgs& a, int grid, int threads, hipStream_t stream);
 hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, int threads, hipStream_t stream);
+hipError_t launch_duplex(const DuplexArgs& x, int grid, hipStream_t stream);  // 1024-thread workgroups
 // Before a decrypt: zeroes its work words and, for an in-place flat decrypt
 // (boundary != NULL), snapshots C[begin-1] of every range that starts inside a payload.
 hipError_t launch_dec_prepass(const DecArgs& a, uint32_t work_words, hipStream_t stream);
@@ -170,8 +183,11 @@ hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long
 // CYAES_CLOCK_PROBE: 8 words).  cyaes_debug_bounds / _probe sum them.
 int bounds_read_enc(unsigned long long* rec4, unsigned int* lines);
 int bounds_read_dec(unsigned long long* rec4, unsigned int* lines);
+int bounds_read_dup(unsigned long long* rec4, unsigned int* lines);
 int probe_read_enc(unsigned long long* out8);
 int probe_read_dec(unsigned long long* out8);
+int probe_read_dup(unsigned long long* out8);
+int timeline_read_dup(int kind, uint4* out);
 int timeline_read_enc(int kind, uint4* out);
 int timeline_read_dec(int kind, uint4* out);
 

@@ -567,25 +567,29 @@ hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long
 // Reads and clears the probe sums of every kernel TU: out[8] = (enc, dec) x
 // {cycles, ticks, waves, max ticks}.
 extern "C" int cyaes_debug_probe(unsigned long long* out) {
-    unsigned long long part[3][8];
-    if (cyaes::read_probe_local(part[0]) || cyaes::probe_read_enc(part[1]) || cyaes::probe_read_dec(part[2])) return -1;
+    unsigned long long part[4][8];
+    if (cyaes::read_probe_local(part[0]) || cyaes::probe_read_enc(part[1]) || cyaes::probe_read_dec(part[2]) ||
+        cyaes::probe_read_dup(part[3]))
+        return -1;
     for (int i = 0; i < 8; i++) {
         out[i] = 0;
-        for (int t = 0; t < 3; t++) out[i] = (i % 4 == 3) ? std::max(out[i], part[t][i]) : out[i] + part[t][i];
+        for (int t = 0; t < 4; t++) out[i] = (i % 4 == 3) ? std::max(out[i], part[t][i]) : out[i] + part[t][i];
     }
     return 0;
 }
 
 // Per-wave timeline of the last launch of a kind (0 encrypt, 1 decrypt) in one
 // kernel translation unit (0: this one -- quad encrypt, ragged decrypt; 1: the
-// lane encrypt; 2: the flat decrypt): kTimelineWaves x 2 uint4 (cyaes_device.h),
-// read and cleared.  tools/timeline.py.
+// lane encrypt; 2: the flat decrypt; 3: the duplex kernel, kind 0 its encrypt
+// phase and kind 1 its decrypt phase): kTimelineWaves x 2 uint4
+// (cyaes_device.h), read and cleared.  tools/timeline.py.
 extern "C" int cyaes_debug_timeline(int tu, int kind, void* out) {
     if (kind < 0 || kind > 1) return -1;
     uint4* o = static_cast<uint4*>(out);
     if (tu == 0) return cyaes::read_timeline_local(kind, o);
     if (tu == 1) return cyaes::timeline_read_enc(kind, o);
     if (tu == 2) return cyaes::timeline_read_dec(kind, o);
+    if (tu == 3) return cyaes::timeline_read_dup(kind, o);
     return -1;
 }
 #endif
@@ -593,22 +597,22 @@ extern "C" int cyaes_debug_timeline(int tu, int kind, void* out) {
 #if CYAES_BOUNDS_CHECK
 // Reads and clears the bounds records of every kernel TU: out[4] = misses, the
 // first miss's source position (TU * 10000 + line: 0 cyaes_kernels.hip, 1
-// cyaes_enc_kernels.hip, 2 cyaes_dec_kernels.hip), its offset from the
-// extent's start, the extent's size; then up to 8 (position, misses) pairs in
-// out[4..20).
+// cyaes_enc_kernels.hip, 2 cyaes_dec_kernels.hip, 3 cyaes_duplex_kernels.hip),
+// its offset from the extent's start, the extent's size; then up to 8
+// (position, misses) pairs in out[4..20).
 extern "C" int cyaes_debug_bounds(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    static unsigned long long rec[3][4];
-    static unsigned int lines[3][cyaes::kBoundsLines];
+    static unsigned long long rec[4][4];
+    static unsigned int lines[4][cyaes::kBoundsLines];
     if (cyaes::read_bounds_local(rec[0], lines[0]) || cyaes::bounds_read_enc(rec[1], lines[1]) ||
-        cyaes::bounds_read_dec(rec[2], lines[2]))
+        cyaes::bounds_read_dec(rec[2], lines[2]) || cyaes::bounds_read_dup(rec[3], lines[3]))
         return -1;
     for (int i = 0; i < 20; i++) out[i] = 0;
-    for (int t = 0; t < 3; t++) {
+    for (int t = 0; t < 4; t++) {
         if (rec[t][0] && !out[0]) out[1] = 10000ull * t + rec[t][1], out[2] = rec[t][2], out[3] = rec[t][3];
         out[0] += rec[t][0];
     }
-    for (uint32_t t = 0, k = 4; t < 3; t++)
+    for (uint32_t t = 0, k = 4; t < 4; t++)
         for (uint32_t l = 0; l < cyaes::kBoundsLines && k < 20; l++)
             if (lines[t][l]) out[k++] = 10000ull * t + l, out[k++] = lines[t][l];
     return 0;

@@ -30,6 +30,8 @@ struct cyaes_gpu {
     uint32_t dec_dyn_pct = kDecDynPct;  // env CYAES_DEC_DYN_PCT: % of a decrypt's work in the dynamic pool
     int dec_grid_max = 0;       // env CYAES_DEC_GRID: cap on decrypt workgroups (tests: many ranges per wave on small batches)
     bool strided_lists = false; // env CYAES_STRIDED_LISTS=1: strided decrypts as ragged batches (tests, A/B)
+    bool duplex_off = false;    // env CYAES_DUPLEX=0: duplex calls run as two launches (tests, A/B)
+    uint32_t duplex_dyn_pct = kDuplexDynPct;  // env CYAES_DUPLEX_DYN_PCT: the duplex decrypt's pool share (%)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
     uint32_t* d_keys = nullptr;    // nkeys * kSchedWords
     uint32_t nkeys = 0;
@@ -159,11 +161,22 @@ namespace {
 
 // offsets == nullptr and stride != 0: a strided batch (payload p at off0 + p *
 // stride, payload_bytes each), run by the ragged kernels without lists.
-int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
-                   uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk,
-                   const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream, const uint32_t* table = nullptr,
-                   uint32_t table_keys = 0, uint64_t off0 = 0, uint64_t stride = 0) {
-    EncArgs a = {};
+// An encrypt batch's arguments and launch shape (encrypt_common launches it;
+// the duplex launch runs its lane walk inside the duplex grid).
+struct EncPlan {
+    EncArgs a;
+    bool quad;     // k_encrypt_quad (latency-bound batch or small ragged one)
+    bool sess;     // SESS grid: a lane per work item, not persistent
+    int grid, threads;
+};
+
+int enc_plan(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
+             uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in,
+             uint8_t* iv_out, const uint32_t* table, uint32_t table_keys, uint64_t off0, uint64_t stride,
+             EncPlan* plan) {
+    EncArgs& a = plan->a;
+    a = EncArgs{};
+    plan->quad = plan->sess = false;
     a.off0 = off0;
     a.stride = stride;
     const bool ragged = offsets != nullptr || stride != 0;
@@ -183,8 +196,10 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
         // Latency-bound batch (fewer chains than lanes to fill the chip four
         // times over), or a ragged one: four lanes per chain (k_encrypt_quad).
         const Shape sh = wave_shape(ctx, (4 * npayloads + 63) / 64, kEncThreads);
-        CY_TRY(launch_encrypt_quad(a, std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
-        return note_key_use(ctx, a.keys.table, stream);
+        plan->quad = true;
+        plan->grid = std::min(sh.grid, enc_grid_cap(ctx));
+        plan->threads = sh.threads;
+        return CYAES_OK;
     }
     // Runs (k_encrypt RUNS): a uniform batch of short payloads with more
     // payloads than the chip has lanes gives each lane R consecutive payloads
@@ -226,8 +241,23 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     // schedule once, before its loop); more workgroups than CUs queue.
     const uint64_t sess_grid = (waves * 64 + sh.threads - 1) / sh.threads;
     if (sess && sess_grid > (uint64_t)INT32_MAX) return CYAES_EINVAL;
-    CY_TRY(launch_encrypt(a, sess ? (int)sess_grid : std::min(sh.grid, enc_grid_cap(ctx)), sh.threads, stream));
-    return note_key_use(ctx, a.keys.table, stream);
+    plan->sess = sess;
+    plan->grid = sess ? (int)sess_grid : std::min(sh.grid, enc_grid_cap(ctx));
+    plan->threads = sh.threads;
+    return CYAES_OK;
+}
+
+int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
+                   uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk,
+                   const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream, const uint32_t* table = nullptr,
+                   uint32_t table_keys = 0, uint64_t off0 = 0, uint64_t stride = 0) {
+    EncPlan plan;
+    int st = enc_plan(ctx, in, out, offsets, nbytes, npayloads, payload_bytes, key_idx, ppk, iv_in, iv_out, table,
+                      table_keys, off0, stride, &plan);
+    if (st) return st;
+    if (plan.quad) CY_TRY(launch_encrypt_quad(plan.a, plan.grid, plan.threads, stream));
+    else CY_TRY(launch_encrypt(plan.a, plan.grid, plan.threads, stream));
+    return note_key_use(ctx, plan.a.keys.table, stream);
 }
 
 // Per-call device scratch (the decrypt's work words and range-boundary
@@ -355,26 +385,42 @@ int alias_iv(cyaes_gpu* ctx, StreamScratch& sc, const uint8_t** iv_in, const uin
 // Uniform batch (off0 = stride = 0: contiguous), or a strided one (payload p at
 // byte off0 + p * stride; unkeyed, no IV arrays, >= 64 blocks per payload, 32-bit
 // payload indices and stride: the callers check).
-int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t npayloads, uint32_t payload_bytes,
-                    const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream,
-                    const uint32_t* table = nullptr, uint32_t table_keys = 0, uint64_t off0 = 0, uint64_t stride = 0) {
-    DecArgs a = {};
+// A flat decrypt's arguments, launch grid and per-launch scratch; the scratch
+// blocks are released (behind the launch's kernels) when the plan goes out of
+// scope.  dyn_pct: -1 the context's choice (long launches only), else the
+// dynamic pool on with that share of the work (the duplex launch).
+struct DecPlan {
+    DecArgs a;
+    int grid;
+    StreamScratch iv_copy, boundary, work;
+};
+
+int dec_plan(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t npayloads, uint32_t payload_bytes,
+             const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream,
+             const uint32_t* table, uint32_t table_keys, uint64_t off0, uint64_t stride, int dyn_pct, int grid_want,
+             DecPlan* plan) {
+    DecArgs& a = plan->a;
+    a = DecArgs{};
     a.off0 = off0;
     a.stride = stride;
-    int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys, table, table_keys);
-    if (st) return st;
+    {
+        const int ks = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys, table, table_keys);
+        if (ks) return ks;
+    }
     if ((iv_in || iv_out) && npayloads > 0xFFFFFFFFull) return CYAES_EINVAL;
     const uint32_t bpp = payload_bytes / 16;
     const uint64_t nblocks = npayloads * bpp;
     const uint64_t step = 64ull * kDecRows;
     const uint64_t waves_needed = (nblocks + step - 1) / step;
     constexpr int kWaves = kDecThreads / 64;
-    const int grid = (int)std::min<uint64_t>((waves_needed + kWaves - 1) / kWaves, (uint64_t)dec_grid_cap(ctx));
+    int grid = (int)std::min<uint64_t>((waves_needed + kWaves - 1) / kWaves, (uint64_t)dec_grid_cap(ctx));
+    if (grid_want > 0) grid = grid_want;  // (the duplex grid: the encrypt's)
+    plan->grid = grid;
     const uint64_t nwaves = (uint64_t)grid * kWaves;
     uint64_t bpw = (nblocks + nwaves - 1) / nwaves;  // the static split: one range per wave
     bpw = (bpw + step - 1) / step * step;
-    StreamScratch iv_copy, boundary, work;
-    st = alias_iv(ctx, iv_copy, &iv_in, iv_out, npayloads, stream);
+    StreamScratch &iv_copy = plan->iv_copy, &boundary = plan->boundary, &work = plan->work;
+    int st = alias_iv(ctx, iv_copy, &iv_in, iv_out, npayloads, stream);
     if (st) return st;
     a.in = in;
     a.out = out;
@@ -400,11 +446,12 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     // Auto: only long launches (> kDecShortSteps steps per wave, config C) take the
     // pool; short ones level their waves by progress feedback alone (r04 A/B:
     // the pool cost config B 2-3 % and gained config C ~1 %).
-    const bool dyn_want = ctx->dec_dyn == 1 || (ctx->dec_dyn < 0 && fair_steps > kDecShortSteps);
+    const bool dyn_want = dyn_pct >= 0 || ctx->dec_dyn == 1 || (ctx->dec_dyn < 0 && fair_steps > kDecShortSteps);
     a.dyn = dyn_want && !keyed_lane && !a.sess_blocks && !iv_in && !iv_out && dyn_steps > 0 &&
             dyn_steps < fair_steps;
     if (a.dyn) {
-        uint64_t stat_steps = fair_steps * (100 - std::min<uint32_t>(ctx->dec_dyn_pct, 100)) / 100;
+        const uint32_t pct = dyn_pct >= 0 ? (uint32_t)dyn_pct : ctx->dec_dyn_pct;
+        uint64_t stat_steps = fair_steps * (100 - std::min<uint32_t>(pct, 100)) / 100;
         while (stat_steps && nwaves * stat_steps * step > nblocks) stat_steps--;
         a.stat_blocks = stat_steps * step;
         a.nstat = stat_steps ? (uint32_t)nwaves : 0;
@@ -445,8 +492,18 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
     // progress words are reset by their workgroups.  A small static batch (the
     // drop-in's packet) launches the kernel alone, as before.
     if (a.dyn || a.boundary) CY_TRY(launch_dec_prepass(a, ww, stream));
-    CY_TRY(launch_decrypt_flat(a, grid, stream));
-    return note_key_use(ctx, a.keys.table, stream);
+    return CYAES_OK;
+}
+
+int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t npayloads, uint32_t payload_bytes,
+                    const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream,
+                    const uint32_t* table = nullptr, uint32_t table_keys = 0, uint64_t off0 = 0, uint64_t stride = 0) {
+    DecPlan plan;
+    int st = dec_plan(ctx, in, out, npayloads, payload_bytes, key_idx, ppk, iv_in, iv_out, stream, table, table_keys,
+                      off0, stride, -1, 0, &plan);
+    if (st) return st;
+    CY_TRY(launch_decrypt_flat(plan.a, plan.grid, stream));
+    return note_key_use(ctx, plan.a.keys.table, stream);
 }
 
 int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
@@ -581,6 +638,8 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* v = getenv("CYAES_DEC_GRID")) ctx->dec_grid_max = atoi(v);
     if (const char* v = getenv("CYAES_DEC_DYN_PCT")) ctx->dec_dyn_pct = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_STRIDED_LISTS")) ctx->strided_lists = atoi(v) != 0;
+    if (const char* v = getenv("CYAES_DUPLEX")) ctx->duplex_off = atoi(v) == 0;
+    if (const char* v = getenv("CYAES_DUPLEX_DYN_PCT")) ctx->duplex_dyn_pct = (uint32_t)strtoul(v, nullptr, 10);
     const HostTables& t = host_tables();
     uint8_t host[kTablesBytes];
     memcpy(host + kEncTableOff, t.enc, sizeof(t.enc));
@@ -883,6 +942,64 @@ int cyaes_gpu_decrypt_strided(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_ou
                               uint32_t payloads_per_key, void* stream) {
     return strided_batch(ctx, true, d_in, d_out, first_offset, stride, npayloads, payload_bytes, d_key_idx,
                          payloads_per_key, (hipStream_t)stream);
+}
+
+// Duplex: one batch encrypted and another decrypted in one launch
+// (cyaes_duplex_kernels.hip).  Falls back to the two ordinary launches, in
+// that order, whenever the duplex grid does not apply: a half too small to
+// fill the GPU on its own (the quad encrypt, or a decrypt without a dynamic
+// pool), or batches whose bytes overlap (the two halves run concurrently).
+static bool overlaps(const uint8_t* a, uint64_t na, const uint8_t* b, uint64_t nb) {
+    return (uintptr_t)a < (uintptr_t)b + nb && (uintptr_t)b < (uintptr_t)a + na;
+}
+
+int cyaes_gpu_duplex_uniform(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d_enc_out, uint64_t enc_npayloads,
+                             uint32_t enc_payload_bytes, uint32_t enc_key, const uint8_t* d_dec_in, uint8_t* d_dec_out,
+                             uint64_t dec_npayloads, uint32_t dec_payload_bytes, uint32_t dec_key, void* stream) {
+    if (!ctx || enc_payload_bytes % 16 || dec_payload_bytes % 16) return CYAES_EINVAL;
+    const bool has_e = enc_npayloads && enc_payload_bytes, has_d = dec_npayloads && dec_payload_bytes;
+    if (has_e && !batch_args_ok(ctx, d_enc_in, d_enc_out, nullptr, nullptr)) return CYAES_EINVAL;
+    if (has_d && !batch_args_ok(ctx, d_dec_in, d_dec_out, nullptr, nullptr)) return CYAES_EINVAL;
+    if ((has_e && enc_key >= ctx->nkeys) || (has_d && dec_key >= ctx->nkeys)) return CYAES_ERANGE;
+    if (!has_e && !has_d) return CYAES_OK;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t* te = ctx->d_keys + (uint64_t)enc_key * kSchedWords;
+    const uint32_t* td = ctx->d_keys + (uint64_t)dec_key * kSchedWords;
+    auto sequential = [&]() -> int {
+        if (has_e) {
+            const int st = encrypt_common(ctx, d_enc_in, d_enc_out, nullptr, nullptr, enc_npayloads, enc_payload_bytes,
+                                          nullptr, 0, nullptr, nullptr, s, te, 1);
+            if (st) return st;
+        }
+        return has_d ? decrypt_uniform(ctx, d_dec_in, d_dec_out, dec_npayloads, dec_payload_bytes, nullptr, 0, nullptr,
+                                       nullptr, s, td, 1)
+                     : CYAES_OK;
+    };
+    if (!has_e || !has_d || ctx->duplex_off) return sequential();
+    const uint64_t eb = enc_npayloads * enc_payload_bytes, db = dec_npayloads * dec_payload_bytes;
+    if (overlaps(d_enc_out, eb, d_dec_in, db) || overlaps(d_enc_out, eb, d_dec_out, db) ||
+        overlaps(d_dec_out, db, d_enc_in, eb))
+        return sequential();
+    EncPlan ep;
+    int st = enc_plan(ctx, d_enc_in, d_enc_out, nullptr, nullptr, enc_npayloads, enc_payload_bytes, nullptr, 0, nullptr,
+                      nullptr, te, 1, 0, 0, &ep);
+    if (st) return st;
+    if (ep.quad || ep.sess || ep.threads != kDecThreads) return sequential();
+    DecPlan dp;
+    st = dec_plan(ctx, d_dec_in, d_dec_out, dec_npayloads, dec_payload_bytes, nullptr, 0, nullptr, nullptr, s, td, 1, 0,
+                  0, (int)ctx->duplex_dyn_pct, ep.grid, &dp);
+    if (st) return st;
+    if (!dp.a.dyn) {  // (its prepass, if any, only zeroed scratch words)
+        CY_TRY(launch_encrypt(ep.a, ep.grid, ep.threads, s));
+        CY_TRY(launch_decrypt_flat(dp.a, dp.grid, s));
+        return note_key_use(ctx, te, s);
+    }
+    DuplexArgs x;
+    x.e = ep.a;
+    x.d = dp.a;
+    CY_TRY(launch_duplex(x, ep.grid, s));
+    return note_key_use(ctx, te, s);
 }
 
 int cyaes_gpu_check(cyaes_gpu* ctx) {

@@ -155,6 +155,26 @@ int cyaes_gpu_cbc_decrypt_batch(cyaes_gpu* ctx, const uint8_t* d_in, uint8_t* d_
                                 const uint32_t* d_nbytes, const uint32_t* d_key_idx, const uint8_t* d_iv,
                                 uint32_t npayloads, void* stream);
 
+/* ---- Duplex: one batch encrypted and another decrypted in ONE launch ------
+ * The relay carries both directions of a pipe at once (relay_server.cpp:472
+ * encrypts target -> tunnel while :329 decrypts tunnel -> target;
+ * relay_local.cpp:206 / :365 on the client).  Same results as
+ *   cyaes_gpu_encrypt_uniform(enc batch, key row enc_key)
+ *   cyaes_gpu_decrypt_uniform(dec batch, key row dec_key)
+ * in that order: uniform contiguous batches, one key each (a row of the key
+ * table), no IV arrays (every payload a chain from DefaultIV), 16-B aligned
+ * buffers, in place allowed.  One grid walks the encrypt batch and then,
+ * workgroup by workgroup, the decrypt batch from a dynamic pool, so the
+ * encrypt's tail (a CBC chain per lane cannot be split; the XCDs' clocks
+ * differ) is filled with decrypt work instead of idling.  Halves too small to
+ * fill the GPU, and batches whose bytes overlap, run as the two ordinary
+ * launches.  Either half may be empty (npayloads or payload_bytes 0).
+ * Errors: CYAES_EINVAL (size % 16, NULL or misaligned buffer), CYAES_ERANGE
+ * (key row >= the number of keys set). */
+int cyaes_gpu_duplex_uniform(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d_enc_out, uint64_t enc_npayloads,
+                             uint32_t enc_payload_bytes, uint32_t enc_key, const uint8_t* d_dec_in, uint8_t* d_dec_out,
+                             uint64_t dec_npayloads, uint32_t dec_payload_bytes, uint32_t dec_key, void* stream);
+
 /* ---- Host-resident uniform batches (PCIe-inclusive) ----------------------
  * The relay path starts and ends in host memory (socket buffers).  These
  * process npayloads uniform payloads that live in HOST memory: chunks of

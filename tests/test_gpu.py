@@ -952,3 +952,108 @@ def test_dropin_size_zero_and_pieces():
     env = dict(os.environ, CYAES_DROPIN_PIECE="4096")
     r = subprocess.run([__import__("sys").executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "pieces ok" in r.stdout, r.stdout + r.stderr
+
+
+# ------------------------------------------------------------ duplex launch --
+def _digest_hex(c, d, nbytes):
+    return ["%016x" % v for v in c.digest(d, nbytes)]
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_duplex_config_b_and_c_goldens(torch, golden, inplace):
+    """cyaes_gpu_duplex_uniform (one grid: encrypt one batch, then decrypt
+    another; relay_server.cpp:472 and :329, the two directions of a pipe):
+    config B encrypted while config C's ciphertext is decrypted, and config C
+    encrypted while B's is decrypted, against the committed OpenSSL digests
+    (B's and C's ciphertext, the plaintexts back), in and out of place."""
+    cfg = golden["openssl"]["configs"]
+    c = ca.GpuContext(0)
+    c.set_keys(K0)
+    sz = {k: (cfg[k]["npayloads"], cfg[k]["payload_bytes"]) for k in ("B", "C")}
+    nb = {k: n * pb for k, (n, pb) in sz.items()}
+    pt = {k: empty(torch, nb[k]) for k in sz}
+    for k, (n, pb) in sz.items():
+        c.fill_synthetic(pt[k], 0, n, pb, oracle.PLAINTEXT_SEED)
+    ct_c = empty(torch, nb["C"])
+    c.encrypt_uniform(pt["C"], ct_c, *sz["C"])
+    assert _digest_hex(c, ct_c, nb["C"]) == cfg["C"]["cipher_digest"]
+    # B encrypted while C's ciphertext is decrypted
+    ct_b = pt["B"] if inplace else empty(torch, nb["B"])
+    rt_c = ct_c if inplace else empty(torch, nb["C"])
+    c.duplex_uniform(pt["B"], ct_b, *sz["B"], ct_c, rt_c, *sz["C"])
+    assert _digest_hex(c, ct_b, nb["B"]) == cfg["B"]["cipher_digest"]
+    assert _digest_hex(c, rt_c, nb["C"]) == cfg["C"]["plain_digest"]
+    # C encrypted while B's ciphertext is decrypted
+    ct_c2 = rt_c if inplace else empty(torch, nb["C"])
+    rt_b = ct_b if inplace else empty(torch, nb["B"])
+    c.duplex_uniform(rt_c, ct_c2, *sz["C"], ct_b, rt_b, *sz["B"])
+    assert _digest_hex(c, ct_c2, nb["C"]) == cfg["C"]["cipher_digest"]
+    assert _digest_hex(c, rt_b, nb["B"]) == cfg["B"]["plain_digest"]
+    assert c.check() == ca.CYAES_OK
+    c.close()
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("shape", ["runs", "big", "small_enc", "small_dec", "overlap", "empty_enc", "empty_dec",
+                                   "off"])
+def test_duplex_shapes_match_separate_launches(torch, shape):
+    """The duplex launch against the two ordinary launches (another context per
+    key row), over the shapes that take the duplex grid (encrypt runs; BIG
+    decrypt payloads; different key rows per half) and the ones that fall back
+    to two launches: a half too small to fill the GPU, overlapping batches (the
+    decrypt reads what the encrypt writes: encrypt-then-decrypt order), an empty
+    half, CYAES_DUPLEX=0."""
+    keys = [K0, oracle.session_key(1), oracle.session_key(2)]
+    env = {"CYAES_DUPLEX": "0"} if shape == "off" else {}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        c = ca.GpuContext(0)
+    finally:
+        _restore(old)
+    c.set_keys(b"".join(keys))
+    ref = [ca.GpuContext(0) for _ in keys]
+    for r, k in zip(ref, keys):
+        r.set_keys(k)
+    en, epb, dn, dpb = {"runs": (1 << 20, 1472, 300000, 1024), "big": (262144, 4096, 20000, 65536),
+                        "small_enc": (5000, 1472, 400000, 1472), "small_dec": (262144, 2048, 100, 1472),
+                        "overlap": (262144, 2048, 262144, 2048), "empty_enc": (0, 1472, 300000, 1472),
+                        "empty_dec": (262144, 2048, 0, 1472), "off": (262144, 2048, 300000, 1472)}[shape]
+    ek, dk = (1, 2) if shape in ("big", "runs") else (0, 0)
+    e_in, e_out = empty(torch, en * epb), empty(torch, en * epb)
+    d_in, d_out = empty(torch, dn * dpb), empty(torch, dn * dpb)
+    if en:
+        c.fill_synthetic(e_in, 7, en, epb, oracle.PLAINTEXT_SEED)
+    if dn:
+        c.fill_synthetic(d_in, 11, dn, dpb, oracle.PLAINTEXT_SEED)  # decrypted as it is: any bytes are a ciphertext
+    if shape == "overlap":  # the decrypt reads the encrypt's output
+        c.duplex_uniform(e_in, e_out, en, epb, e_out, d_out, dn, dpb)
+        assert torch.equal(d_out, e_in)  # encrypt, then decrypt of its output
+        want_e = empty(torch, en * epb)
+        ref[0].encrypt_uniform(e_in, want_e, en, epb)
+        assert torch.equal(e_out, want_e)
+    else:
+        c.duplex_uniform(e_in, e_out, en, epb, d_in, d_out, dn, dpb, enc_key=ek, dec_key=dk)
+        if en:
+            want_e = empty(torch, en * epb)
+            ref[ek].encrypt_uniform(e_in, want_e, en, epb)
+            assert torch.equal(e_out, want_e)
+        if dn:
+            want_d = empty(torch, dn * dpb)
+            ref[dk].decrypt_uniform(d_in, want_d, dn, dpb)
+            assert torch.equal(d_out, want_d)
+    # spot checks against the oracle
+    torch.cuda.synchronize()
+    if en:
+        p = en // 3
+        want = oracle.batch(False, [keys[ek]], 0, oracle.synthetic(7 + p, 1, epb), epb)
+        assert np.array_equal(e_out[p * epb:(p + 1) * epb].cpu().numpy(), want)
+    assert c.check() == ca.CYAES_OK
+    with pytest.raises(ca.CyaesError):  # key row out of range
+        c.duplex_uniform(e_in, e_out, max(en, 1), epb, d_in, d_out, dn, dpb, enc_key=3)
+    with pytest.raises(ca.CyaesError):  # size % 16
+        c.duplex_uniform(e_in, e_out, max(en, 1), epb + 4, d_in, d_out, dn, dpb)
+    for r in ref:
+        r.close()
+    c.close()
+    torch.cuda.empty_cache()

@@ -11,7 +11,11 @@ launch's tail the waves of a few slow CUs / XCDs (a dynamic work split helps)
 or uniform (it does not).
 
 usage: python tools/timeline.py [--config B|C|D|relay] [--lib build/variants/clockprobe.so]
-       [--reps 3] [ENV=VALUE ...]   (context settings, e.g. CYAES_DEC_DYN=0)
+       [--reps 3] [--duplex] [ENV=VALUE ...]   (context settings, e.g. CYAES_DEC_DYN=0)
+--duplex: one duplex launch (cyaes_gpu_duplex_uniform: the config's encrypt and,
+in the same grid, the decrypt of its ciphertext) instead of the two launches;
+its encrypt and decrypt phases are reported on one clock (the launch's first
+wave start).
 """
 import argparse
 import ctypes
@@ -24,10 +28,10 @@ sys.path.insert(0, ROOT)
 WAVES = 8192
 
 
-def records(lib, kind):
+def records(lib, kind, tus=(0, 1, 2)):
     """Timeline records of the last launch of `kind` (0 enc, 1 dec) from whichever kernel TU ran it."""
     out = []
-    for tu in (0, 1, 2):
+    for tu in tus:
         buf = (ctypes.c_uint32 * (8 * WAVES))()
         if lib.cyaes_debug_timeline(tu, kind, buf) != 0:
             raise SystemExit("cyaes_debug_timeline failed (not a clock-probe build?)")
@@ -40,11 +44,12 @@ def records(lib, kind):
     return out
 
 
-def report(name, recs):
+def report(name, recs, t0=None):
     if not recs:
         print("%s: no records" % name)
         return
-    t0 = min(r["start"] for r in recs)
+    if t0 is None:
+        t0 = min(r["start"] for r in recs)
     for r in recs:  # 32-bit tick counters: relative to the launch's first start (wraps every 42 s)
         r["s"] = ((r["start"] - t0) & 0xFFFFFFFF) / 1e5  # ms
         r["e"] = ((r["end"] - t0) & 0xFFFFFFFF) / 1e5
@@ -90,6 +95,7 @@ def main():
     ap.add_argument("--config", default="B", choices=["B", "C", "D", "relay"])
     ap.add_argument("--lib", default=os.path.join(ROOT, "build", "variants", "clockprobe.so"))
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--duplex", action="store_true")
     ap.add_argument("env", nargs="*")
     args = ap.parse_args()
     for kv in args.env:
@@ -124,6 +130,23 @@ def main():
         enc()
         dec()
     torch.cuda.synchronize()
+    if args.duplex:
+        ct2 = torch.empty_like(pt)
+        for rep in range(args.reps):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            c.duplex_uniform(pt, ct2, n, pb, ct, rt, n, pb, stream=s)  # encrypt pt while ct is decrypted
+            ev[1].record()
+            torch.cuda.synchronize()
+            re_, rd = records(lib, 0, (3,)), records(lib, 1, (3,))
+            t0 = min(r["start"] for r in re_)
+            print("== config %s rep %d: duplex launch %.3f ms (events) %s" % (
+                args.config, rep, ev[0].elapsed_time(ev[1]), " ".join(args.env)))
+            report("duplex encrypt phase", re_, t0)
+            report("duplex decrypt phase", rd, t0)
+        assert torch.equal(rt, pt) and torch.equal(ct2, ct)
+        c.close()
+        return
     for rep in range(args.reps):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         ev[0].record()
