@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--payloads", type=int, default=0, help="A-D: override payloads per GPU")
     ap.add_argument("--e-pass-payloads", type=int, default=E_PASS_PAYLOADS, help="E: payloads per pass")
     ap.add_argument("--e-passes", type=int, default=E_PASSES, help="E: passes in the whole job")
+    ap.add_argument("--e-mode", default="duplex", choices=["duplex", "sequential"],
+                    help="E: duplex = launch j encrypts pass j while it decrypts pass j-1 (cyaes_gpu_duplex_uniform); "
+                         "sequential = an encrypt and a decrypt launch per pass")
     ap.add_argument("--cpu-sample", type=int, default=0, help="cpu baseline sample payloads (0 = auto)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
@@ -119,10 +122,12 @@ def traffic_plan(traffic, rank, world, config, environ):
 def live_traffic(timeout_s=150):
     """HBM bytes per AES launch, measured now: two rocprofv3 --pmc passes
     (FETCH_SIZE, WRITE_SIZE; one counter each, as MI355X_MICROARCH.md's
-    HBM section prescribes) over `bench.py --config C --steps 2`, each a child
+    HBM section prescribes) over `bench.py --config E --e-passes 2 --steps 1`
+    (config C-sized passes: an encrypt launch, a duplex launch, a decrypt
+    launch, plus the encrypt that leaves pass 0 for the e2e check), each a child
     process with its own time limit.  Corrections as tools/traffic.py: kB x1024,
-    FETCH_SIZE x2 on gfx950.  Returns ({"encrypt": bytes, "decrypt": bytes}, None)
-    or (None, reason)."""
+    FETCH_SIZE x2 on gfx950.  Returns ({"encrypt": bytes, "decrypt": bytes,
+    "duplex": bytes}, None) or (None, reason)."""
     import shutil
     import signal
     import subprocess
@@ -139,9 +144,9 @@ def live_traffic(timeout_s=150):
             # rocprofv3 is a python script: run it with this interpreter, so the
             # only exec is rocprofv3's own of the profiled program
             cmd = [sys.executable, prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
-                   sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C", "--steps", "2", "--warmup", "0",
-                   "--no-cpu", "--no-verify", "--no-clock", "--packet-configs", "none", "--relay-stream", "0",
-                   "--e2e-gib", "0", "--traffic", "none"]
+                   sys.executable, os.path.join(ROOT, "bench.py"), "--config", "E", "--e-passes", "2", "--steps", "1",
+                   "--warmup", "0", "--no-cpu", "--no-verify", "--no-clock", "--packet-configs", "none",
+                   "--relay-stream", "0", "--e2e-gib", "0", "--traffic", "none"]
             env = dict(os.environ)
             for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
                 env.pop(k, None)
@@ -531,11 +536,12 @@ def main():
             raise SystemExit("config E: %d passes do not split over %d ranks" % (passes, world))
         mine = list(range(rank * passes // world, (rank + 1) * passes // world))
         nbytes = pp * pb
+        duplex = args.e_mode == "duplex"
         set_session_keys(0, pp, 0)
-        log("rank %d/%d: config E, passes %d..%d of %d, %d payloads x %d B = %.2f GiB per pass, %d CUs"
-            % (rank, world, mine[0], mine[-1], passes, pp, pb, nbytes / gib, ctx.num_cus))
+        log("rank %d/%d: config E, passes %d..%d of %d, %d payloads x %d B = %.2f GiB per pass, %d CUs, %s launches"
+            % (rank, world, mine[0], mine[-1], passes, pp, pb, nbytes / gib, ctx.num_cus, args.e_mode))
         d_pt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-        d_ct = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        d_cts = [torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(2 if duplex else 1)]
         d_rt = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
         gfile = os.path.join(ROOT, "tests", "golden", "config_e_passes.json")
         gpass = {}
@@ -547,25 +553,71 @@ def main():
         def fill(i):
             ctx.fill_synthetic(d_pt, i * pp, pp, pb, PLAINTEXT_SEED, sh)
 
-        def enc():
-            ctx.encrypt_uniform(d_pt, d_ct, pp, pb, stream=sh)
+        def walk(ev, verify_walk):
+            """One walk of this rank's passes.  Sequential: per pass, an encrypt
+            launch and a decrypt launch.  Duplex: launch j encrypts pass j while
+            it decrypts pass j-1 (cyaes_gpu_duplex_uniform; the two directions of
+            a relay pipe, relay_server.cpp:472 / :329), plus a decrypt-only
+            launch after the last pass.  Each pass's plaintext is written into
+            HBM first (untimed input staging); every launch is timed between
+            device synchronisations.  Returns (timed s, fill s, verified passes, ok)."""
+            t_aes = t_fill = 0.0
+            verified, ok = [], True
+            prev = None  # (pass, its ciphertext buffer, its plaintext digest)
 
-        def dec():
-            ctx.decrypt_uniform(d_ct, d_rt, pp, pb, stream=sh)
+            def timed(*launches):  # (kind, fn) ...: back to back, one timed segment
+                nonlocal t_aes
+                torch.cuda.synchronize()
+                a0 = time.perf_counter()
+                for rec, fn in launches:
+                    if ev is not None:
+                        ev.append((rec, torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                        ev[-1][1].record(stream)
+                    fn()
+                    if ev is not None:
+                        ev[-1][2].record(stream)
+                torch.cuda.synchronize()
+                t_aes += time.perf_counter() - a0
 
-        verified, ok = [], True
-        for w in range(max(warmup, 1 if verify else 0)):
-            for i in mine:
-                fill(i)
-                enc()
-                dec()
-                if verify and w == 0:
-                    good = ctx.digest(d_rt, nbytes, sh) == ctx.digest(d_pt, nbytes, sh)
+            for j, i in enumerate(mine):
+                f0 = time.perf_counter()
+                fill(i)  # input staging: the pass's payloads arrive in HBM (untimed)
+                torch.cuda.synchronize()
+                t_fill += time.perf_counter() - f0
+                pdig = ctx.digest(d_pt, nbytes, sh) if verify_walk else None
+                ct = d_cts[j % len(d_cts)]
+                if duplex and prev is not None:
+                    pct = prev[1]
+                    timed(("duplex", lambda: ctx.duplex_uniform(d_pt, ct, pp, pb, pct, d_rt, pp, pb, stream=sh)))
+                elif duplex:
+                    timed(("encrypt", lambda: ctx.encrypt_uniform(d_pt, ct, pp, pb, stream=sh)))
+                else:
+                    timed(("encrypt", lambda: ctx.encrypt_uniform(d_pt, ct, pp, pb, stream=sh)),
+                          ("decrypt", lambda: ctx.decrypt_uniform(ct, d_rt, pp, pb, stream=sh)))
+                if verify_walk:
+                    good = True
+                    if duplex and prev is not None:  # the previous pass came back in this launch
+                        good = ctx.digest(d_rt, nbytes, sh) == prev[2]
+                    elif not duplex:
+                        good = ctx.digest(d_rt, nbytes, sh) == pdig
                     if i in gpass:
-                        good = good and digests_match(gpass[i], d_pt, d_ct, nbytes)
+                        good = good and digests_match(gpass[i], d_pt, ct, nbytes)
                         if good:
                             verified.append(i)
                     ok = ok and good
+                prev = (i, ct, pdig)
+            if duplex:  # the last pass's decrypt
+                pct = prev[1]
+                timed(("decrypt", lambda: ctx.decrypt_uniform(pct, d_rt, pp, pb, stream=sh)))
+                if verify_walk:
+                    ok = ok and ctx.digest(d_rt, nbytes, sh) == prev[2]
+            return t_aes, t_fill, verified, ok
+
+        verified, ok = [], True
+        for w in range(max(warmup, 1 if verify else 0)):
+            _, _, v, good = walk(None, verify and w == 0)
+            if verify and w == 0:
+                verified, ok = v, good
         torch.cuda.synchronize()
         parity = None
         if verify:
@@ -573,28 +625,16 @@ def main():
             parity = "bit-exact" if all_ok(ok) else "MISMATCH"
             log("config E parity: %s (golden passes verified on rank %d: %s)" % (parity, rank, verified))
 
-        ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-                torch.cuda.Event(enable_timing=True)) for _ in mine] for _ in range(steps)]
+        ev = []
         t_aes, t_fill = 0.0, 0.0
         if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         t_begin = time.perf_counter()
-        for s in range(steps):
-            for j, i in enumerate(mine):
-                f0 = time.perf_counter()
-                fill(i)  # input staging: the pass's payloads arrive in HBM (untimed)
-                torch.cuda.synchronize()
-                a0 = time.perf_counter()
-                ev[s][j][0].record(stream)
-                enc()
-                ev[s][j][1].record(stream)
-                dec()
-                ev[s][j][2].record(stream)
-                torch.cuda.synchronize()
-                a1 = time.perf_counter()
-                t_fill += a0 - f0
-                t_aes += a1 - a0
+        for _ in range(steps):
+            ta, tf, _, _ = walk(ev, False)
+            t_aes += ta
+            t_fill += tf
         torch.cuda.synchronize()
         if dist_on:
             dist.barrier()
@@ -606,21 +646,24 @@ def main():
         if dist_on:
             shards = [None] * world
             dist.all_gather_object(shards, shard)
-        n = steps * len(mine)
+
+        def avg(kind):
+            v = [a.elapsed_time(b) for k, a, b in ev if k == kind]
+            return sum(v) / len(v) if v else None
         res = {
             "name": "E", "npay": pp, "pb": pb, "ppk": 0, "nbytes": nbytes, "t": t, "steps": steps,
             "value": 2.0 * nbytes * passes * steps / t / gib,
-            "enc_ms": sum(a.elapsed_time(b) for row in ev for a, b, _ in row) / n,
-            "dec_ms": sum(b.elapsed_time(c) for row in ev for _, b, c in row) / n,
-            "parity": parity, "d_ct": d_ct, "d_pt": d_pt, "passes_per_gpu": len(mine), "passes": passes,
+            "enc_ms": avg("encrypt"), "dec_ms": avg("decrypt"), "duplex_ms": avg("duplex"),
+            "launches": {k: sum(1 for e in ev if e[0] == k) // steps for k in ("encrypt", "decrypt", "duplex")},
+            "parity": parity, "d_ct": d_cts[0], "d_pt": d_pt, "passes_per_gpu": len(mine), "passes": passes,
             "fill_ms": max_over_ranks(t_fill) / steps * 1e3, "wall_ms": max_over_ranks(t_wall) / steps * 1e3,
             "shards": shards,
         }
-        # leave pass 0's plaintext and cipher in d_pt / d_ct for the e2e check and the cpu baseline
-        # sample (rank 0 walks pass 0 at every N)
+        # leave pass 0's plaintext and cipher in d_pt / d_cts[0] for the e2e check and the cpu
+        # baseline sample (rank 0 walks pass 0 at every N)
         if rank == 0 and mine[0] == 0:
             fill(0)
-            enc()
+            ctx.encrypt_uniform(d_pt, d_cts[0], pp, pb, stream=sh)
         del d_rt
         return res
 
@@ -632,6 +675,7 @@ def main():
     nbytes, pb, ppk = main_res["nbytes"], main_res["pb"], main_res["ppk"]
     npay, t, value = main_res["npay"], main_res["t"], main_res["value"]
     enc_ms, dec_ms, parity = main_res["enc_ms"], main_res["dec_ms"], main_res["parity"]
+    dup_ms = main_res.get("duplex_ms")  # config E in duplex mode: the launches that hold 32/N - 1 of the passes
 
     # In-kernel shader clock under this load: the clock-probe build of the same
     # kernels on the same buffers (s_memtime cycles / s_memrealtime 100 MHz ticks
@@ -657,6 +701,18 @@ def main():
         plib.cyaes_debug_probe(buf)
         clock = {k: (buf[4 * i] / buf[4 * i + 1] * 0.1 if buf[4 * i + 1] else None)
                  for i, k in enumerate(("encrypt", "decrypt"))}
+        if dup_ms:  # the duplex launch: its encrypt and decrypt phases together, cycles over ticks
+            d_ct2 = torch.empty_like(d_tmp)
+            for r in range(3):
+                pctx.encrypt_uniform(main_res["d_pt"], d_tmp, npay, pb, stream=sh)  # the decrypt half's input
+                torch.cuda.synchronize()
+                plib.cyaes_debug_probe(buf)  # (discarded)
+                pctx.duplex_uniform(main_res["d_pt"], d_ct2, npay, pb, d_tmp, d_tmp, npay, pb, stream=sh)
+                torch.cuda.synchronize()
+                plib.cyaes_debug_probe(buf)  # this duplex launch: kind 0 its encrypt phase, kind 1 its decrypt
+            cyc, tick = buf[0] + buf[4], buf[1] + buf[5]
+            clock["duplex"] = cyc / tick * 0.1 if tick else None
+            del d_ct2
         pctx.close()
         del d_tmp
 
@@ -678,26 +734,34 @@ def main():
                        achieved=round(per_clk, 2), frac=round(per_clk / LDS_LANES_PER_CLK_CU, 4))
         return out
 
-    kern = {k: dict(roof(ms), avg_ms=round(ms, 4), ceiling=ceiling(ms, (clock or {}).get(k)))
-            for k, ms in (("encrypt", enc_ms), ("decrypt", dec_ms))}
-    dom = "encrypt" if enc_ms >= dec_ms else "decrypt"
-    roofline = dict(roof(enc_ms if dom == "encrypt" else dec_ms), kernel=dom, traffic=None,
+    # Per kernel: algorithmic bytes per launch (encrypt / decrypt: N read + N
+    # written; duplex: both, 4N) over its average launch time (HIP events on the
+    # launch stream).  Config E in duplex mode: the duplex launches carry 31 of
+    # 32 passes' work, so they are the dominant kernel.
+    launches = [("encrypt", enc_ms, 1), ("decrypt", dec_ms, 1)] + ([("duplex", dup_ms, 2)] if dup_ms else [])
+    kern = {k: dict(roof(ms, nbytes * m), avg_ms=round(ms, 4), algorithmic_bytes=int(2 * nbytes * m),
+                    ceiling=ceiling(ms, (clock or {}).get(k), nbytes * m))
+            for k, ms, m in launches if ms}
+    dom = "duplex" if dup_ms else ("encrypt" if enc_ms >= dec_ms else "decrypt")
+    roofline = dict(roof(kern[dom]["avg_ms"], nbytes * (2 if dup_ms else 1)), kernel=dom, traffic=None,
                     ceiling=kern[dom]["ceiling"])
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     ftr = None
     if os.path.exists(tfile):
         ftr = json.load(open(tfile)).get("C" if args.config == "E" else args.config, {}).get(dom)
     if live and dom in live:
-        algo = 2.0 * CONFIGS["C"][0] * CONFIGS["C"][1]  # the passes profile config C's launches (live_traffic)
+        algo1 = 2.0 * CONFIGS["C"][0] * CONFIGS["C"][1]  # the passes profile config C-sized launches (live_traffic)
+        algo = {"duplex": 2 * algo1}
         roofline["traffic"] = live[dom]
         roofline["traffic_note"] = ("measured in this run: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes (separate "
-                                    "child processes, bench.py --config C --steps 2), FETCH_SIZE x2 per the gfx950 "
-                                    "calibration, x1024 kB->B; per launch of the dominant kernel")
-        roofline["traffic_ratio"] = round(live[dom] / algo, 4)
+                                    "child processes, bench.py --config E --e-passes 2, i.e. config C-sized launches: "
+                                    "an encrypt, a duplex, a decrypt), FETCH_SIZE x2 per the gfx950 calibration, "
+                                    "x1024 kB->B; per launch of the dominant kernel")
+        roofline["traffic_ratio"] = round(live[dom] / algo.get(dom, algo1), 4)
         for k in kern:
             if k in live:
                 kern[k]["traffic"] = live[k]
-                kern[k]["traffic_ratio"] = round(live[k] / algo, 4)
+                kern[k]["traffic_ratio"] = round(live[k] / algo.get(k, algo1), 4)
     elif ftr and args.traffic != "none":
         roofline["traffic"] = ftr.get("bytes_per_launch")
         roofline["traffic_note"] = "committed profiles/traffic.json (%s); " % (why,) + str(ftr.get("note"))
@@ -858,9 +922,14 @@ def main():
                            same_keys_all_ranks=len({sh["keys_sha256_16"] for sh in main_res["shards"]}) == 1)
         if args.config == "E":
             out["config"].update(passes=main_res["passes"], passes_per_gpu=main_res["passes_per_gpu"])
-            out["timing"] = {"timed": "per pass: encrypt + decrypt between device synchronisations, summed; "
-                                      "max over ranks", "fill_ms_per_step": round(main_res["fill_ms"], 3),
-                             "wall_ms_per_step_incl_fill": round(main_res["wall_ms"], 3)}
+            out["config"].update(launches=args.e_mode)
+            timed = ("per pass: the pass's launches between device synchronisations (duplex: launch j encrypts "
+                     "pass j and decrypts pass j-1, plus one decrypt launch after the last pass), summed; max over "
+                     "ranks" if args.e_mode == "duplex" else
+                     "per pass: encrypt + decrypt between device synchronisations, summed; max over ranks")
+            out["timing"] = {"timed": timed, "fill_ms_per_step": round(main_res["fill_ms"], 3),
+                             "wall_ms_per_step_incl_fill": round(main_res["wall_ms"], 3),
+                             "launches_per_step": main_res.get("launches")}
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()

@@ -56,7 +56,6 @@ struct cyaes_gpu {
     // exactly those streams, not for the device.
     std::mutex key_mu;
     std::vector<std::pair<hipStream_t, hipEvent_t>> key_uses;
-    hipStream_t key_stream = nullptr;     // private, non-blocking: the table's host-side writes and reads
     hipEvent_t keys_written = nullptr;    // behind cyaes_gpu_set_keys_device's expansion on the caller's stream
     bool keys_written_pending = false;
     std::vector<uint32_t*> retired_keys;  // tables outgrown while batches may still read them; freed at destroy
@@ -650,7 +649,6 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_status), 16);
     if (e == hipSuccess) e = hipMemset(ctx->d_status, 0, 16);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_digest), 16);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->key_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->keys_written, hipEventDisableTiming);
     if (e != hipSuccess) {
         cyaes_gpu_destroy(ctx);
@@ -680,7 +678,6 @@ int cyaes_gpu_destroy(cyaes_gpu* ctx) {
     }
     for (auto& u : ctx->key_uses) (void)hipEventDestroy(u.second);
     if (ctx->keys_written) (void)hipEventDestroy(ctx->keys_written);
-    if (ctx->key_stream) (void)hipStreamDestroy(ctx->key_stream);
     delete ctx;
     return map_err(e);
 }
@@ -688,6 +685,21 @@ int cyaes_gpu_destroy(cyaes_gpu* ctx) {
 int cyaes_gpu_device(const cyaes_gpu* ctx) { return ctx ? ctx->device : -1; }
 int cyaes_gpu_num_cus(const cyaes_gpu* ctx) { return ctx ? ctx->num_cus : 0; }
 uint32_t cyaes_gpu_nkeys(const cyaes_gpu* ctx) { return ctx ? ctx->nkeys : 0; }
+
+// A private non-blocking stream for one key-table copy, destroyed after it.
+// Not kept in the context: the box gives a process 4 hardware queues
+// (GPU_MAX_HW_QUEUES) and streams beyond that share them, so a context-lifetime
+// stream here made the host pipe's upload and compute streams share a queue
+// (e2e encrypt 42.8 -> 31.9 GiB/s, back to 43.5 with 8 queues;
+// profiles/r05/e2e_hw_queues.txt).
+struct KeyStream {
+    hipStream_t s = nullptr;
+    hipError_t e;
+    KeyStream() { e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking); }
+    ~KeyStream() {
+        if (s) (void)hipStreamDestroy(s);
+    }
+};
 
 // The key table's writers wait only for the streams that read it: each
 // stream's last batch under this context's table (note_key_use), and an
@@ -717,10 +729,11 @@ static int reserve_keys(cyaes_gpu* ctx, uint32_t nkeys, uint32_t keep_rows, bool
     CY_TRY(hipMalloc(reinterpret_cast<void**>(&t), (uint64_t)cap * kSchedWords * 4));
     if (keep_rows) {
         int st = wait_key_writes(ctx);
-        hipError_t e = st ? hipErrorUnknown
-                          : hipMemcpyAsync(t, ctx->d_keys, (uint64_t)keep_rows * kSchedWords * 4,
-                                           hipMemcpyDeviceToDevice, ctx->key_stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(ctx->key_stream);
+        KeyStream ks;
+        hipError_t e = st ? hipErrorUnknown : ks.e;
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(t, ctx->d_keys, (uint64_t)keep_rows * kSchedWords * 4, hipMemcpyDeviceToDevice, ks.s);
+        if (e == hipSuccess) e = hipStreamSynchronize(ks.s);
         if (e != hipSuccess) {
             (void)hipFree(t);
             return st ? st : map_err(e);
@@ -742,9 +755,11 @@ static int write_key_rows(cyaes_gpu* ctx, uint32_t first, const uint32_t* host, 
     }
     int st = wait_key_writes(ctx);
     if (st) return st;
+    KeyStream ks;
+    CY_TRY(ks.e);
     CY_TRY(hipMemcpyAsync(ctx->d_keys + (uint64_t)first * kSchedWords, host, (uint64_t)n * kSchedWords * 4,
-                          hipMemcpyHostToDevice, ctx->key_stream));
-    CY_TRY(hipStreamSynchronize(ctx->key_stream));
+                          hipMemcpyHostToDevice, ks.s));
+    CY_TRY(hipStreamSynchronize(ks.s));
     return CYAES_OK;
 }
 
@@ -813,9 +828,10 @@ int cyaes_gpu_get_key(cyaes_gpu* ctx, uint32_t index, cyaes_key* out) {
     uint32_t w[kSchedWords];
     int st = wait_key_writes(ctx);
     if (st) return st;
-    CY_TRY(hipMemcpyAsync(w, ctx->d_keys + (uint64_t)index * kSchedWords, sizeof(w), hipMemcpyDeviceToHost,
-                          ctx->key_stream));
-    CY_TRY(hipStreamSynchronize(ctx->key_stream));
+    KeyStream ks;
+    CY_TRY(ks.e);
+    CY_TRY(hipMemcpyAsync(w, ctx->d_keys + (uint64_t)index * kSchedWords, sizeof(w), hipMemcpyDeviceToHost, ks.s));
+    CY_TRY(hipStreamSynchronize(ks.s));
     from_device_schedule(w, out);
     return CYAES_OK;
 }

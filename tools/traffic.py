@@ -30,7 +30,8 @@ def per_launch_kb(d, counter):
             if row["Counter_Name"] != counter:
                 continue
             name = row["Kernel_Name"]
-            kind = "encrypt" if "k_encrypt" in name else "decrypt" if "k_decrypt" in name else None
+            kind = ("encrypt" if "k_encrypt" in name else "decrypt" if "k_decrypt" in name else
+                    "duplex" if "k_duplex" in name else None)
             if kind is None:
                 continue
             sums[kind] += float(row["Counter_Value"])
@@ -47,12 +48,13 @@ def main():
     fetch = per_launch_kb(a.fetch_dir, "FETCH_SIZE")
     write = per_launch_kb(a.write_dir, "WRITE_SIZE")
     out = {"C": {}}
-    for k in ("encrypt", "decrypt"):
+    for k in [k for k in ("encrypt", "decrypt", "duplex") if k in fetch and k in write]:
         fb = int(round(fetch[k] * 1024 * 2))
         wb = int(round(write[k] * 1024))
         out["C"][k] = {
             "bytes_per_launch": fb + wb, "fetch_bytes": fb, "write_bytes": wb,
-            "algorithmic_bytes": ALGO, "ratio": round((fb + wb) / ALGO, 4),
+            "algorithmic_bytes": ALGO * (2 if k == "duplex" else 1),
+            "ratio": round((fb + wb) / (ALGO * (2 if k == "duplex" else 1)), 4),
             "raw": {"FETCH_SIZE_kB_per_launch": fetch[k], "WRITE_SIZE_kB_per_launch": write[k]},
             "note": NOTE,
         }
