@@ -210,8 +210,10 @@ def test_bench_line_contract_single_gpu():
     r = out["roofline"]
     assert r["bound"] == "lds" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3 and r["traffic"] > 0
-    # the live PMC passes price config C's pass kernels alone (no e2e chunk launches mixed into the average)
-    assert 0.95 < r["traffic_ratio"] < 1.1, r
+    # the live PMC passes price config C-sized launches alone (no e2e chunk launches mixed into the average);
+    # the product kernels only (a variant build such as the bounds-checked one reads its extents too)
+    if not os.environ.get("CYAES_LIBRARY"):
+        assert 0.95 < r["traffic_ratio"] < 1.1, r
     c = out["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["matches_gpu"] is True and c["sample"]
     b = out["packet_configs"]["B"]

@@ -11,6 +11,7 @@
 #   bench      python bench.py (default: config E headline + packet configs + relay stream)
 #   quickbench bench.py --steps 3 --warmup 1 (no CPU baseline)
 #   profile    rocprofv3 --kernel-trace --stats of a short bench, then FETCH_SIZE / WRITE_SIZE PMC passes
+#              (config E, 2 passes: an encrypt, a duplex and a decrypt launch of config C's size)
 #   cfgtest    tests/test_config_e.py only (bench.py's own contract and multi-rank runs)
 #   pytest:F   tests/F (a file or file::test), -m gpu
 #   batchertest  tests/test_batcher.py only
@@ -54,7 +55,7 @@ for step in "$@"; do
         -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --packet-configs none --relay-stream 0 --e2e-gib 0 --traffic none) || exit $?
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && run pmc_$c 300 rocprofv3 --pmc $c -d "$O/pmc_$c" -o run --output-format csv \
-          -- python3 "$R/bench.py" --config C --steps 2 --warmup 0 --no-cpu --no-verify --no-clock \
+          -- python3 "$R/bench.py" --config E --e-passes 2 --steps 1 --warmup 0 --no-cpu --no-verify --no-clock \
              --packet-configs none --relay-stream 0 --e2e-gib 0 --traffic none) || exit $?
       done ;;
     cfgtest) run pytest_config_e 400 python -u -m pytest tests/test_config_e.py -m gpu -x -v --timeout 150 --timeout-method thread ;;

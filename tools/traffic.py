@@ -14,7 +14,8 @@ import os
 from collections import defaultdict
 
 ALGO = 2 * 262144 * 65536     # config C: read N + write N bytes per launch
-NOTE = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py config C; "
+NOTE = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py config E with 2 passes (config "
+        "C-sized encrypt, duplex and decrypt launches); "
         "FETCH_SIZE x2 per the gfx950 calibration, x1024 kB->B")
 
 
