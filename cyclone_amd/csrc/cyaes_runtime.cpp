@@ -266,13 +266,10 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
 // handed out again only once its event has completed.  So batches of one
 // context on different streams never share a block while a kernel still
 // reads it, and nothing is freed before the context is destroyed.
-// (Until late r04 the blocks came from a private hipMemPool with
-// hipMallocFromPoolAsync / hipFreeAsync.  Twice in r04's GPU runs a torch
-// host-to-device copy right after one context was destroyed (its pool with
-// it) and the next created failed with an illegal address, with no kernel
-// of this library launched since a device-wide synchronisation: the pool's
-// deferred release is the suspect, so the library no longer uses the
-// stream-ordered allocator)
+// (Until late r04 the blocks came from a private hipMemPool.  r04 blamed that
+// pool for two illegal-address reports on torch host-to-device copies; r05
+// traced them to host registrations instead (a registration that outlives
+// its memory).  The plain hipMalloc blocks stayed.)
 constexpr size_t kScratchMaxBlocks = 64;             // beyond this, reuse a pending block behind its event
 constexpr uint64_t kScratchCacheBytes = 256ull << 20;  // above this, completed blocks are freed, largest first
 
