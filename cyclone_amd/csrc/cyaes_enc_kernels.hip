@@ -21,7 +21,24 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
     enc_body<RAGGED, KEYED, RUNS, SESS>(a, reinterpret_cast<const char*>(lds_words), &lead);
 }
 
+// Strided batches of whole 1,024-payload groups read by 64-B lines
+// (cyaes_enc_body.h, enc_lines_body).
+__global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_lines(EncArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
+    fill_enc_image(lds_words, a.tables);
+    __shared__ uint32_t lead;  // prio_feedback
+    if (threadIdx.x == 0) lead = 0;
+    __syncthreads();
+    CLOCK_PROBE(0);
+    enc_lines_body(a, reinterpret_cast<const char*>(lds_words), &lead);
+}
+
 }  // namespace
+
+hipError_t launch_encrypt_lines(const EncArgs& a, int grid, int threads, hipStream_t stream) {
+    hipLaunchKernelGGL(k_encrypt_lines, dim3(grid), dim3(threads), 0, stream, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;

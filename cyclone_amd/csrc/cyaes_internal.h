@@ -163,6 +163,9 @@ struct DuplexArgs {
 
 // Launchers (cyaes_*kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t stream);
+// Strided, unkeyed, no IV arrays, npayloads a multiple of kLinesGroup (k_encrypt_lines).
+constexpr uint64_t kLinesGroup = 1024;
+hipError_t launch_encrypt_lines(const EncArgs& a, int grid, int threads, hipStream_t stream);
 // Four lanes per chain (latency-bound batches; threads a multiple of 64).
 hipError_t launch_encrypt_quad(const EncArgs& a, int grid, int threads, hipStream_t stream);
 hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream);

@@ -24,6 +24,8 @@ struct cyaes_gpu {
     uint32_t ragged_group = 0;  // env CYAES_RAGGED_GROUP: payloads per ragged-decrypt wave group (0 = auto; tests, A/B)
     uint32_t enc_run = 0;       // env CYAES_ENC_RUN: payloads per lane run of the uniform encrypt (0 = auto; tests, A/B)
     bool enc_no_sess = false;   // env CYAES_ENC_NO_SESS=1: keyed uniform encrypt always by waterfall (tests, A/B)
+    bool enc_no_lines = false;  // env CYAES_ENC_LINES=0: strided encrypts without k_encrypt_lines (tests, A/B)
+    int enc_lines_grid = 0;     // env CYAES_ENC_LINES_GRID: cap on k_encrypt_lines' grid (tests: several items per wave)
     int dec_dyn = -1;           // env CYAES_DEC_DYN: 1 / 0 force the dynamic decrypt pool on / off; -1: long launches only
     uint32_t dec_range_steps = kDecRangeSteps;  // env CYAES_DEC_RANGE_STEPS: steps per dynamic flat-decrypt range
     uint32_t dec_groups_per_wave = kDecGroupsPerWave;  // env CYAES_DEC_GROUPS_PER_WAVE: ragged groups per wave
@@ -254,6 +256,24 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     int st = enc_plan(ctx, in, out, offsets, nbytes, npayloads, payload_bytes, key_idx, ppk, iv_in, iv_out, table,
                       table_keys, off0, stride, &plan);
     if (st) return st;
+    // A strided batch for the lane kernel, unkeyed and without IV arrays: its
+    // whole 1,024-payload groups are read by 64-B lines (k_encrypt_lines), the
+    // rest (if any) by the ordinary plan.
+    // The kernel's offsets from the stream base are 32-bit (lines reach <= 63 B past a payload).
+    const uint64_t nlines_pay = npayloads / kLinesGroup * kLinesGroup;
+    const bool span32 = nlines_pay && (nlines_pay - 1) * stride + payload_bytes + off0 + 64 <= 0xFFFFFFFFull;
+    if (stride && !offsets && !key_idx && !ppk && !iv_in && !iv_out && !plan.quad && span32 && !ctx->enc_no_lines) {
+        EncArgs la = plan.a;
+        la.npayloads = nlines_pay;
+        const Shape sh = wave_shape(ctx, nlines_pay / 64, kEncThreads);
+        int grid = std::min(sh.grid, enc_grid_cap(ctx));
+        if (ctx->enc_lines_grid > 0) grid = std::min(grid, ctx->enc_lines_grid);
+        CY_TRY(launch_encrypt_lines(la, grid, sh.threads, stream));
+        st = note_key_use(ctx, la.keys.table, stream);
+        if (st || nlines_pay == npayloads) return st;
+        return encrypt_common(ctx, in, out, nullptr, nullptr, npayloads - nlines_pay, payload_bytes, nullptr, 0,
+                              nullptr, nullptr, stream, table, table_keys, off0 + nlines_pay * stride, stride);
+    }
     if (plan.quad) CY_TRY(launch_encrypt_quad(plan.a, plan.grid, plan.threads, stream));
     else CY_TRY(launch_encrypt(plan.a, plan.grid, plan.threads, stream));
     return note_key_use(ctx, plan.a.keys.table, stream);
@@ -628,6 +648,8 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* g = getenv("CYAES_RAGGED_GROUP")) ctx->ragged_group = (uint32_t)strtoul(g, nullptr, 10);
     if (const char* r = getenv("CYAES_ENC_RUN")) ctx->enc_run = (uint32_t)strtoul(r, nullptr, 10);
     if (const char* v = getenv("CYAES_ENC_NO_SESS")) ctx->enc_no_sess = atoi(v) != 0;
+    if (const char* v = getenv("CYAES_ENC_LINES")) ctx->enc_no_lines = atoi(v) == 0;
+    if (const char* v = getenv("CYAES_ENC_LINES_GRID")) ctx->enc_lines_grid = atoi(v);
     if (const char* v = getenv("CYAES_DEC_DYN")) ctx->dec_dyn = atoi(v) != 0 ? 1 : 0;
     if (const char* v = getenv("CYAES_DEC_RANGE_STEPS")) ctx->dec_range_steps = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_DEC_GROUPS_PER_WAVE")) ctx->dec_groups_per_wave = (uint32_t)strtoul(v, nullptr, 10);

@@ -863,6 +863,62 @@ def test_device_relay_stream_strided(chunk, mode):
     ctx.close()
 
 
+@pytest.mark.parametrize("pb,stride,first,inplace", [
+    (1472, 1484, 12, True), (1472, 1484, 12, False),  # relay packets: 4 line phases (12 + 12 p mod 64)
+    (1472, 1476, 60, True),                           # phases 60 + 4 p: all 16
+    (4080, 4092, 12, False), (64, 76, 4, True),       # 255 and 4 blocks
+    (16, 20, 8, False),                               # one block per payload
+    (1456, 1520, 16, True), (1472, 1536, 0, True),    # 16-B phases (no dword shift), line-aligned
+])
+def test_strided_encrypt_by_lines(pb, stride, first, inplace):
+    """Strided encrypts read by 64-B lines (k_encrypt_lines, cyaes_enc_body.h):
+    whole 1,024-payload groups by lines, the rest by the ragged lane / quad
+    kernels; every payload a chain from DefaultIV (relay_local.cpp:206), at
+    payload phases 0-60 B in the line, in place and out of place.  Bit-exact
+    against the oracle and against the same context type without the lines
+    kernel (CYAES_ENC_LINES=0); a 3-workgroup grid walks several items per
+    wave (each item's first chunk loaded during the previous one's last); the
+    bytes around the payloads are untouched."""
+    import numpy as np
+    import torch
+    n = 2 * 1024 + 437
+    key = _keys(1, 83)[0]
+    rng = np.random.default_rng(83)
+    plain = rng.integers(0, 256, n * pb, dtype=np.uint8)
+    want = oracle.batch(False, [key], 0, plain, pb)
+    size = first + (n - 1) * stride + pb + 3
+    ctxs = []
+    for env in ({"CYAES_QUAD_MAX_CHAINS": "1024"}, {"CYAES_QUAD_MAX_CHAINS": "1024", "CYAES_ENC_LINES_GRID": "3"},
+                {"CYAES_QUAD_MAX_CHAINS": "1024", "CYAES_ENC_LINES": "0"}):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        ctxs.append(ca.GpuContext(0))
+        for k, v in old.items():
+            os.environ.pop(k) if v is None else os.environ.__setitem__(k, v)
+    outs = []
+    for ctx in ctxs:
+        ctx.set_keys(key)
+        src = torch.full((size,), 0xA7, dtype=torch.uint8, device="cuda")
+        view = src[first: first + n * stride - (stride - pb)].as_strided((n, pb), (stride, 1))
+        view.copy_(torch.from_numpy(plain.reshape(n, pb)).cuda())
+        before = src.clone()
+        dst = src if inplace else torch.full_like(src, 0x3C)
+        ctx.encrypt_strided(src, dst, first, stride, n, pb)
+        torch.cuda.synchronize()
+        got = dst[first: first + n * stride - (stride - pb)].as_strided((n, pb), (stride, 1)).cpu().numpy()
+        assert np.array_equal(got.reshape(-1), want), "payloads differ from the oracle"
+        mask = torch.ones(size, dtype=torch.bool, device="cuda")
+        mask[first: first + n * stride - (stride - pb)].as_strided((n, pb), (stride, 1)).fill_(False)
+        around = dst[mask]
+        assert bool((around == (before[mask] if inplace else 0x3C)).all()), "bytes outside the payloads changed"
+        if not inplace:
+            assert torch.equal(src, before), "input stream changed"
+        assert ctx.check() == ca.CYAES_OK
+        outs.append(dst.cpu())
+        ctx.close()
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2])
+
+
 def test_strided_stream_beyond_4gib():
     """A strided stream spanning more than 4 GiB (three 2,048-B payloads 2 GiB
     + 16 B apart): the flat decrypt's strided rows use 32-bit offsets, so the

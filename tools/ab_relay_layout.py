@@ -7,7 +7,7 @@ cyaes_gpu_{en,de}crypt_strided)
 one property at a time: packet stride (payload + header bytes), payload offset
 inside the packet (12 = relay, 16 = 16-B aligned) and in place vs a separate
 output stream.  usage: python tools/ab_relay_layout.py [--n 1048576] [--pb 1472]
-[--lib a.so [b.so ...]] [--layouts relay_inplace,...]  (several libs: interleaved per round, one process)"""
+[--lib a.so[:ENV=V] [b.so ...]] [--layouts relay_inplace,...]  (several libs: interleaved per round, one process)"""
 import argparse
 import os
 import statistics
@@ -31,7 +31,20 @@ def main():
     import torch
     import cyclone_amd as ca
     libs = args.lib or [None]
-    ctxs = [ca.GpuContext(0, lib=ca.load_library(os.path.abspath(p)) if p else None) for p in libs]
+    ctxs = []
+    for spec in libs:  # path[:ENV=V...]: the environment the context is created under (CYAES_* switches)
+        path, *envs = (spec or "").split(":")
+        saved = {}
+        for kv in envs:
+            k, v = kv.split("=", 1)
+            saved[k] = os.environ.get(k)
+            os.environ[k] = v
+        ctxs.append(ca.GpuContext(0, lib=ca.load_library(os.path.abspath(path)) if path else None))
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
     for c in ctxs:
         c.set_keys(bytes(range(16)))
     c = ctxs[0]
@@ -93,7 +106,7 @@ def main():
         for k, p in enumerate(libs):
             print("%-22s %8d x %5d B stride %5d: enc %.4f ms (min %.4f) dec %.4f ms (min %.4f)  %s  %s" %
                   (label, n, pb, stride, statistics.median(ts[k]), min(ts[k]), statistics.median(td[k]), min(td[k]),
-                   "ok" if ok[k] else "MISMATCH", os.path.basename(p) if p else ""), flush=True)
+                   "ok" if ok[k] else "MISMATCH", p or ""), flush=True)
         del src, dst
         torch.cuda.empty_cache()
 
