@@ -39,7 +39,8 @@ HSRC     := cyclone_amd/csrc/cyaes_runtime.cpp cyclone_amd/csrc/cyaes_pins.cpp c
             cyclone_amd/csrc/cyaes_relay.cpp cyclone_amd/csrc/cyaes_batcher.cpp
 HDRS     := include/cyaes.h include/cyaes_relay.h include/cyaes_batch.h include/cyclone_amd/cyr_rijndael.h cyclone_amd/csrc/cyaes_internal.h \
             cyclone_amd/csrc/cyaes_tables.h
-KHDRS    := $(HDRS) cyclone_amd/csrc/cyaes_device.h cyclone_amd/csrc/cyaes_enc_body.h cyclone_amd/csrc/cyaes_dec_body.h
+KHDRS    := $(HDRS) cyclone_amd/csrc/cyaes_device.h cyclone_amd/csrc/cyaes_enc_body.h cyclone_amd/csrc/cyaes_dec_body.h \
+            cyclone_amd/csrc/cyaes_lines_body.h
 
 KOBJ     := $(BUILD)/cyaes_kernels.o $(BUILD)/cyaes_enc_kernels.o $(BUILD)/cyaes_dec_kernels.o $(BUILD)/cyaes_duplex_kernels.o
 AOBJ     := $(BUILD)/cyaes_adler.o

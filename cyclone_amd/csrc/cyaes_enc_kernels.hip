@@ -2,10 +2,11 @@
 // (k_encrypt; cyr_rijndael.cpp:588-609 + _encryptBlock :638-705).  Compiled
 // with the iterative ILP scheduler (Makefile SCHED_ENC): config C encrypt
 // -1.5 %, B -1.3 % (profiles/r03/ab_sched.txt); the design notes are in
-// cyaes_kernels.hip and DESIGN.md §3.2.
+// cyaes_kernels.hip and DESIGN.md §3.2.  Also the relay-stream encrypt that
+// reads 64-B lines (k_encrypt_lines).
 
 #define CYAES_TU 1
-#include "cyaes_enc_body.h"
+#include "cyaes_lines_body.h"
 
 namespace cyaes {
 namespace {
@@ -22,7 +23,7 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
 }
 
 // Strided batches of whole 1,024-payload groups read by 64-B lines
-// (cyaes_enc_body.h, enc_lines_body).
+// (cyaes_lines_body.h).
 __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_lines(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
     fill_enc_image(lds_words, a.tables);
@@ -30,8 +31,9 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_lines(EncArgs a) {
     if (threadIdx.x == 0) lead = 0;
     __syncthreads();
     CLOCK_PROBE(0);
-    enc_lines_body(a, reinterpret_cast<const char*>(lds_words), &lead);
+    lines_walk(a, reinterpret_cast<const char*>(lds_words), &lead);
 }
+
 
 }  // namespace
 
@@ -39,6 +41,7 @@ hipError_t launch_encrypt_lines(const EncArgs& a, int grid, int threads, hipStre
     hipLaunchKernelGGL(k_encrypt_lines, dim3(grid), dim3(threads), 0, stream, a);
     return hipGetLastError();
 }
+
 
 hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;

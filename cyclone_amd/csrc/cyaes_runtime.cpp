@@ -25,7 +25,7 @@ struct cyaes_gpu {
     uint32_t enc_run = 0;       // env CYAES_ENC_RUN: payloads per lane run of the uniform encrypt (0 = auto; tests, A/B)
     bool enc_no_sess = false;   // env CYAES_ENC_NO_SESS=1: keyed uniform encrypt always by waterfall (tests, A/B)
     bool enc_no_lines = false;  // env CYAES_ENC_LINES=0: strided encrypts without k_encrypt_lines (tests, A/B)
-    int enc_lines_grid = 0;     // env CYAES_ENC_LINES_GRID: cap on k_encrypt_lines' grid (tests: several items per wave)
+    int lines_grid = 0;         // env CYAES_LINES_GRID: cap on k_encrypt_lines' grid (tests: several items per wave)
     int dec_dyn = -1;           // env CYAES_DEC_DYN: 1 / 0 force the dynamic decrypt pool on / off; -1: long launches only
     uint32_t dec_range_steps = kDecRangeSteps;  // env CYAES_DEC_RANGE_STEPS: steps per dynamic flat-decrypt range
     uint32_t dec_groups_per_wave = kDecGroupsPerWave;  // env CYAES_DEC_GROUPS_PER_WAVE: ragged groups per wave
@@ -267,7 +267,7 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
         la.npayloads = nlines_pay;
         const Shape sh = wave_shape(ctx, nlines_pay / 64, kEncThreads);
         int grid = std::min(sh.grid, enc_grid_cap(ctx));
-        if (ctx->enc_lines_grid > 0) grid = std::min(grid, ctx->enc_lines_grid);
+        if (ctx->lines_grid > 0) grid = std::min(grid, ctx->lines_grid);
         CY_TRY(launch_encrypt_lines(la, grid, sh.threads, stream));
         st = note_key_use(ctx, la.keys.table, stream);
         if (st || nlines_pay == npayloads) return st;
@@ -649,7 +649,7 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* r = getenv("CYAES_ENC_RUN")) ctx->enc_run = (uint32_t)strtoul(r, nullptr, 10);
     if (const char* v = getenv("CYAES_ENC_NO_SESS")) ctx->enc_no_sess = atoi(v) != 0;
     if (const char* v = getenv("CYAES_ENC_LINES")) ctx->enc_no_lines = atoi(v) == 0;
-    if (const char* v = getenv("CYAES_ENC_LINES_GRID")) ctx->enc_lines_grid = atoi(v);
+    if (const char* v = getenv("CYAES_LINES_GRID")) ctx->lines_grid = atoi(v);
     if (const char* v = getenv("CYAES_DEC_DYN")) ctx->dec_dyn = atoi(v) != 0 ? 1 : 0;
     if (const char* v = getenv("CYAES_DEC_RANGE_STEPS")) ctx->dec_range_steps = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_DEC_GROUPS_PER_WAVE")) ctx->dec_groups_per_wave = (uint32_t)strtoul(v, nullptr, 10);

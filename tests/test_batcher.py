@@ -871,14 +871,14 @@ def test_device_relay_stream_strided(chunk, mode):
     (1456, 1520, 16, True), (1472, 1536, 0, True),    # 16-B phases (no dword shift), line-aligned
 ])
 def test_strided_encrypt_by_lines(pb, stride, first, inplace):
-    """Strided encrypts read by 64-B lines (k_encrypt_lines, cyaes_enc_body.h):
+    """Strided encrypts read by 64-B lines (k_encrypt_lines, cyaes_lines_body.h):
     whole 1,024-payload groups by lines, the rest by the ragged lane / quad
     kernels; every payload a chain from DefaultIV (relay_local.cpp:206), at
     payload phases 0-60 B in the line, in place and out of place.  Bit-exact
-    against the oracle and against the same context type without the lines
-    kernel (CYAES_ENC_LINES=0); a 3-workgroup grid walks several items per
-    wave (each item's first chunk loaded during the previous one's last); the
-    bytes around the payloads are untouched."""
+    against the oracle and against a context without the lines kernel
+    (CYAES_ENC_LINES=0); a 3-workgroup grid walks several items per wave (each
+    item's first chunk loaded during the previous one's last); the bytes around
+    the payloads are untouched; the stream decrypts back (relay_server.cpp:329)."""
     import numpy as np
     import torch
     n = 2 * 1024 + 437
@@ -888,7 +888,7 @@ def test_strided_encrypt_by_lines(pb, stride, first, inplace):
     want = oracle.batch(False, [key], 0, plain, pb)
     size = first + (n - 1) * stride + pb + 3
     ctxs = []
-    for env in ({"CYAES_QUAD_MAX_CHAINS": "1024"}, {"CYAES_QUAD_MAX_CHAINS": "1024", "CYAES_ENC_LINES_GRID": "3"},
+    for env in ({"CYAES_QUAD_MAX_CHAINS": "1024"}, {"CYAES_QUAD_MAX_CHAINS": "1024", "CYAES_LINES_GRID": "3"},
                 {"CYAES_QUAD_MAX_CHAINS": "1024", "CYAES_ENC_LINES": "0"}):
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
@@ -913,8 +913,16 @@ def test_strided_encrypt_by_lines(pb, stride, first, inplace):
         assert bool((around == (before[mask] if inplace else 0x3C)).all()), "bytes outside the payloads changed"
         if not inplace:
             assert torch.equal(src, before), "input stream changed"
-        assert ctx.check() == ca.CYAES_OK
         outs.append(dst.cpu())
+        # and back: the ciphertext stream decrypted (in place, or into a fresh output stream)
+        back = dst if inplace else torch.full_like(dst, 0x5D)
+        ctx.decrypt_strided(dst, back, first, stride, n, pb)
+        torch.cuda.synchronize()
+        got = back[first: first + n * stride - (stride - pb)].as_strided((n, pb), (stride, 1)).cpu().numpy()
+        assert np.array_equal(got.reshape(-1), plain), "decrypt differs from the plaintext"
+        around = back[mask]
+        assert bool((around == (before[mask] if inplace else 0x5D)).all()), "bytes outside the payloads changed"
+        assert ctx.check() == ca.CYAES_OK
         ctx.close()
     assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2])
 
