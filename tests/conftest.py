@@ -18,6 +18,18 @@ def pytest_configure(config):
         subprocess.run(["make", "-C", ROOT, "-j8", "lib", "oracle"], check=True)
 
 
+def pytest_report_header(config):
+    """Which build of the library this session tests (CYAES_LIBRARY selects a
+    variant; the bounds-checked build exports cyaes_debug_bounds)."""
+    import cyclone_amd
+    path = cyclone_amd.LIB_PATH
+    try:
+        bounds = hasattr(cyclone_amd.load_library(), "cyaes_debug_bounds")  # (torch's HIP runtime first)
+    except (OSError, ImportError) as e:
+        return "cyaes library: %s (not loadable: %s)" % (path, e)
+    return "cyaes library: %s (%s)" % (os.path.relpath(path, ROOT), "bounds-checked build" if bounds else "product build")
+
+
 @pytest.fixture(autouse=True)
 def _gpu_fault_guard(request):
     """After every `gpu` test: synchronise the device, so an asynchronous fault
