@@ -7,8 +7,11 @@ generator and forces the kernel choice through the runtime's A/B knobs:
   decrypt  CYAES_RAGGED_GROUP      payloads per wave group of the ragged kernel
            CYAES_DEC_GRID / CYAES_DEC_RANGE_STEPS / CYAES_DEC_DYN   work ranges from the
            ticket counter on a small grid, or the static per-wave split
-Layouts: uniform (flat decrypt, incl. the session-aligned keyed path) and
-ragged relay-packet streams (payload at packet offset 12, gaps, empties).
+Layouts: uniform (flat decrypt, incl. the session-aligned keyed path),
+ragged relay-packet streams (payload at packet offset 12, gaps, empties) and
+strided streams of equal payloads (cyaes_gpu_{en,de}crypt_strided: any 4-B
+phase and gap; k_encrypt_lines for whole 1,024-payload groups, also on a
+capped grid, CYAES_LINES_GRID; no IV arrays in that API).
 Semantics: Rijndael::encrypt/decrypt per payload (cyr_rijndael.cpp:588-635),
 IV in/out per payload, in place allowed."""
 import os
@@ -60,10 +63,14 @@ def context(env):
 
 def draw_case(seed):
     rng = np.random.default_rng(1000 + seed)
-    layout = rng.choice(["uniform", "ragged"])
+    layout = rng.choice(["uniform", "ragged", "strided"])
     n = int(rng.choice([1, 7, 63, 64, 65, 300, 1000, 2500]))
+    if layout == "strided":
+        n = int(rng.choice([1, 63, 1024, 2100, 3072]))
     if layout == "uniform":
         blocks = np.full(n, int(rng.choice([1, 3, 8, 9, 15, 16, 23, 92, 256, 300])), dtype=np.uint32)
+    elif layout == "strided":
+        blocks = np.full(n, int(rng.choice([1, 4, 8, 9, 23, 92, 100])), dtype=np.uint32)
     else:
         blocks = rng.choice([0, 1, 2, 5, 7, 8, 9, 16, 63, 64, 65, 92, 257], n).astype(np.uint32)
         blocks[rng.integers(0, n, max(1, n // 200))] = int(rng.choice([600, 4080]))
@@ -71,8 +78,10 @@ def draw_case(seed):
     ppk = int(rng.choice([1, 2, 7, 16, 64])) if keying == "ppk" else 0
     return dict(
         rng=rng, layout=layout, n=n, blocks=blocks, keying=keying, ppk=ppk,
-        iv_in=bool(rng.integers(0, 2)), iv_out=bool(rng.integers(0, 2)), inplace=bool(rng.integers(0, 2)),
+        iv_in=bool(rng.integers(0, 2)) and layout != "strided", iv_out=bool(rng.integers(0, 2)) and layout != "strided",
+        inplace=bool(rng.integers(0, 2)), first=4 * int(rng.integers(0, 17)), gap=4 * int(rng.integers(0, 21)),
         env={"CYAES_QUAD_MAX_CHAINS": str(rng.choice(["0", str(1 << 40)])) if rng.integers(0, 3) else None,
+             "CYAES_LINES_GRID": str(rng.choice([1, 3, 7])) if rng.integers(0, 3) == 0 else None,
              "CYAES_RAGGED_GROUP": str(rng.choice([1, 2, 5, 64])) if rng.integers(0, 3) else None,
              # decrypt work distribution: a small grid with 1- or 3-step ticket ranges, or the static split
              "CYAES_DEC_GRID": str(rng.choice([1, 2, 5])) if rng.integers(0, 2) else None,
@@ -97,6 +106,10 @@ def test_batch_sweep(torch, seed):
     if k["layout"] == "uniform":
         offsets = np.arange(n, dtype=np.uint64) * int(sizes[0])
         total = int(n * int(sizes[0]))
+    elif k["layout"] == "strided":
+        stride = int(sizes[0]) + k["gap"]
+        offsets = k["first"] + np.arange(n, dtype=np.uint64) * stride
+        total = k["first"] + (n - 1) * stride + int(sizes[0])
     else:
         offsets = np.zeros(n, dtype=np.uint64)
         pos = 0
@@ -126,6 +139,8 @@ def test_batch_sweep(torch, seed):
         d_ct = d_pt if k["inplace"] else dev(torch, plain)  # out starts as a copy: gaps keep their bytes
         if k["layout"] == "uniform":
             c.encrypt_uniform(d_pt, d_ct, n, int(sizes[0]), iv_in=d_ivi, iv_out=d_ivo, **kw)
+        elif k["layout"] == "strided":
+            c.encrypt_strided(d_pt, d_ct, k["first"], int(sizes[0]) + k["gap"], n, int(sizes[0]), **kw)
         else:
             d_off, d_nb = dev(torch, offsets), dev(torch, sizes)
             c.encrypt_ragged(d_pt, d_ct, d_off, d_nb, n, iv_in=d_ivi, iv_out=d_ivo, **kw)
@@ -139,6 +154,8 @@ def test_batch_sweep(torch, seed):
         d_ivo2 = torch.zeros(n * 16, dtype=torch.uint8, device="cuda") if k["iv_out"] else None
         if k["layout"] == "uniform":
             c.decrypt_uniform(d_src, d_back, n, int(sizes[0]), iv_in=d_ivi, iv_out=d_ivo2, **kw)
+        elif k["layout"] == "strided":
+            c.decrypt_strided(d_src, d_back, k["first"], int(sizes[0]) + k["gap"], n, int(sizes[0]), **kw)
         else:
             c.decrypt_ragged(d_src, d_back, d_off, d_nb, n, iv_in=d_ivi, iv_out=d_ivo2, **kw)
         assert np.array_equal(host(d_back)[:total], plain[:total]), k
