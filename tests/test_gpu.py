@@ -923,6 +923,57 @@ def test_encrypt_whole_wave_sessions_and_runs(torch, run, pb, ppk, nk):
     c.close()
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_duplex_sweep(torch, seed):
+    """Seeded duplex launches (cyaes_gpu_duplex_uniform): random
+    halves (sizes, payload lengths from one block to 64 KiB, key rows, in
+    place or not) under random pool shares and range sizes of the decrypt phase
+    (CYAES_DUPLEX_DYN_PCT, CYAES_DEC_RANGE_STEPS), against the two ordinary
+    launches of reference contexts, bit-exact, and the round trip."""
+    rng = np.random.default_rng(4000 + seed)
+    keys = [K0, oracle.session_key(3), oracle.session_key(4)]
+    epb = int(rng.choice([16, 64, 1472, 4096]))
+    en = int(rng.choice([131072, 200003, 262144, 300000])) if epb <= 1472 else int(rng.choice([131072, 180000]))
+    dpb = int(rng.choice([16, 1024, 1472, 65536]))
+    dn = int(rng.choice([1000, 50000, 262144])) if dpb <= 1472 else int(rng.choice([257, 4000]))
+    ek, dk = int(rng.integers(0, 3)), int(rng.integers(0, 3))
+    e_inplace, d_inplace = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+    env = {"CYAES_DUPLEX_DYN_PCT": str(rng.choice([10, 25, 50, 100])),
+           "CYAES_DEC_RANGE_STEPS": str(rng.choice([1, 4, 16]))}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        c = ca.GpuContext(0)
+    finally:
+        _restore(old)
+    c.set_keys(b"".join(keys))
+    ref = [ca.GpuContext(0) for _ in keys]
+    for r, k in zip(ref, keys):
+        r.set_keys(k)
+    e_in, d_in = empty(torch, en * epb), empty(torch, dn * dpb)
+    c.fill_synthetic(e_in, 3, en, epb, oracle.PLAINTEXT_SEED)
+    c.fill_synthetic(d_in, 5, dn, dpb, oracle.PLAINTEXT_SEED)
+    want_e, want_d = empty(torch, en * epb), empty(torch, dn * dpb)
+    ref[ek].encrypt_uniform(e_in, want_e, en, epb)
+    ref[dk].decrypt_uniform(d_in, want_d, dn, dpb)
+    e_src, d_src = e_in.clone(), d_in.clone()
+    e_out = e_in if e_inplace else empty(torch, en * epb)
+    d_out = d_in if d_inplace else empty(torch, dn * dpb)
+    c.duplex_uniform(e_in, e_out, en, epb, d_in, d_out, dn, dpb, enc_key=ek, dec_key=dk)
+    assert torch.equal(e_out, want_e), (en, epb, ek, env)
+    assert torch.equal(d_out, want_d), (dn, dpb, dk, env)
+    back = empty(torch, en * epb)
+    ref[ek].decrypt_uniform(e_out, back, en, epb)
+    assert torch.equal(back, e_src)
+    if not d_inplace:
+        assert torch.equal(d_in, d_src)
+    assert c.check() == ca.CYAES_OK
+    for r in ref:
+        r.close()
+    c.close()
+    torch.cuda.empty_cache()
+
+
 def test_dropin_size_zero_and_pieces():
     """The drop-in's argument rules: size 0 is a no-op whatever the
     pointers (the reference's loop never runs, cyr_rijndael.cpp:600), and a call
