@@ -91,6 +91,19 @@ __device__ __forceinline__ uint32_t srow(const DecArgs& a, FlatPos ps, uint32_t 
     return o;
 }
 
+// Cost probe (CYAES_PROBE_DEC_ALIGN bit 1: loads, bit 2: stores; wrong
+// output): the row's accesses moved to one contiguous 1-KiB run from lane
+// 0's address rounded down to 64 B, i.e. what line-aligned rows would cost.
+#ifndef CYAES_PROBE_DEC_ALIGN
+#define CYAES_PROBE_DEC_ALIGN 0
+#endif
+template <int BIT, typename P>
+__device__ __forceinline__ P* probe_dec_addr(P* base, uint32_t o, uint32_t lane) {
+    if (!(CYAES_PROBE_DEC_ALIGN & BIT)) return base + o;
+    const uint64_t r0 = reinterpret_cast<uint64_t>(base + __builtin_amdgcn_readfirstlane(o)) & ~63ull;
+    return reinterpret_cast<P*>(r0 + 16ull * lane);
+}
+
 // Loads the R rows of the step at `base` (c); partial steps also load each
 // block's predecessor (pv), full steps take it from the neighbour lane.
 // FULL: all 64*R blocks are in range (every step but possibly the batch's
@@ -104,7 +117,7 @@ __device__ __forceinline__ void flat_load(const DecArgs& a, const uint8_t* in_s,
     const Ext ie = data_ext(a.in, a, STRIDED);
     if (FULL && STRIDED) {  // in_s = in + off0
 #pragma unroll
-        for (int k = 0; k < R; k++) c[k] = LD16U(in_s + srow<BIG>(a, ps, lane, k, rk, pk), ie);
+        for (int k = 0; k < R; k++) c[k] = LD16U(probe_dec_addr<1>(in_s, srow<BIG>(a, ps, lane, k, rk, pk), lane), ie);
     } else if (FULL) {
         const uint8_t* g0 = a.in + 16 * (base + lane);
 #pragma unroll
@@ -252,7 +265,7 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
     }
     if (FULL && STRIDED) {
 #pragma unroll
-        for (int k = 0; k < R; k++) ST16U(out_s + srow<BIG>(a, ps, lane, k, rk, pk), oe, d[k]);
+        for (int k = 0; k < R; k++) ST16U(probe_dec_addr<2>(out_s, srow<BIG>(a, ps, lane, k, rk, pk), lane), oe, d[k]);
     } else if (FULL) {
         uint8_t* o0 = a.out + 16 * (base + lane);
 #pragma unroll
