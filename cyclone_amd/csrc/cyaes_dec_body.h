@@ -264,6 +264,13 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
         }
     }
     if (FULL && STRIDED) {
+        // A scheduling boundary between the rounds and the row addresses: in one
+        // region with them, the per-row address arithmetic tipped the scheduler
+        // into a low-pressure schedule that issues the rounds' LDS reads 4-7 at
+        // a time (318 s_waitcnt per 640 reads against 53 in 64-read bursts), and
+        // the strided step ran 4-5 % slower than the contiguous one on the same
+        // bytes (profiles/r05/ab_dec_sched_barrier.txt).
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < R; k++) ST16U(probe_dec_addr<2>(out_s, srow<BIG>(a, ps, lane, k, rk, pk), lane), oe, d[k]);
     } else if (FULL) {

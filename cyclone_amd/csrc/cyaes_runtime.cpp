@@ -32,6 +32,7 @@ struct cyaes_gpu {
     uint32_t dec_dyn_pct = kDecDynPct;  // env CYAES_DEC_DYN_PCT: % of a decrypt's work in the dynamic pool
     int dec_grid_max = 0;       // env CYAES_DEC_GRID: cap on decrypt workgroups (tests: many ranges per wave on small batches)
     bool strided_lists = false; // env CYAES_STRIDED_LISTS=1: strided decrypts as ragged batches (tests, A/B)
+    bool strided_force = false; // env CYAES_STRIDED_FORCE=1: contiguous strided batches keep the strided kernels (A/B)
     bool duplex_off = false;    // env CYAES_DUPLEX=0: duplex calls run as two launches (tests, A/B)
     uint32_t duplex_dyn_pct = kDuplexDynPct;  // env CYAES_DUPLEX_DYN_PCT: the duplex decrypt's pool share (%)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
@@ -656,6 +657,7 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* v = getenv("CYAES_DEC_GRID")) ctx->dec_grid_max = atoi(v);
     if (const char* v = getenv("CYAES_DEC_DYN_PCT")) ctx->dec_dyn_pct = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_STRIDED_LISTS")) ctx->strided_lists = atoi(v) != 0;
+    if (const char* v = getenv("CYAES_STRIDED_FORCE")) ctx->strided_force = atoi(v) != 0;
     if (const char* v = getenv("CYAES_DUPLEX")) ctx->duplex_off = atoi(v) == 0;
     if (const char* v = getenv("CYAES_DUPLEX_DYN_PCT")) ctx->duplex_dyn_pct = (uint32_t)strtoul(v, nullptr, 10);
     const HostTables& t = host_tables();
@@ -942,7 +944,7 @@ static int strided_batch(cyaes_gpu* ctx, bool decrypt, const uint8_t* in, uint8_
     DeviceGuard g(ctx->device);
     const uint32_t bpp = payload_bytes / 16;
     // Back-to-back payloads, 16-B aligned: a contiguous uniform batch
-    if (stride == payload_bytes && batch_args_ok(ctx, in + first, out + first, nullptr, nullptr))
+    if (stride == payload_bytes && !ctx->strided_force && batch_args_ok(ctx, in + first, out + first, nullptr, nullptr))
         return decrypt ? decrypt_uniform(ctx, in + first, out + first, npayloads, payload_bytes, key_idx, ppk, nullptr,
                                          nullptr, stream)
                        : encrypt_common(ctx, in + first, out + first, nullptr, nullptr, npayloads, payload_bytes,

@@ -30,6 +30,11 @@ def main():
     ap.add_argument("--ppk", type=int, default=0, help="payloads per session key (0: one key)")
     ap.add_argument("--key-idx", action="store_true", help="with --ppk: the same sessions as a per-payload index array")
     ap.add_argument("--relay", action="store_true", help="relay packet stream in place (ragged kernels)")
+    ap.add_argument("--flush-between", action="store_true",
+                    help="overwrite a 1-GiB scratch tensor between the encrypt and the decrypt (evicts the caches; "
+                         "the decrypt is timed from after it)")
+    ap.add_argument("--sync-between", action="store_true",
+                    help="device synchronisation between the encrypt and the decrypt launch (the decrypt starts idle)")
     ap.add_argument("--relay-api", default="ragged", choices=["ragged", "strided"],
                     help="--relay: the ragged entry points (device lists) or the strided ones")
     args = ap.parse_args()
@@ -79,6 +84,9 @@ def main():
             c.encrypt_uniform(pt, ct, n, pb, key_idx=kidx, payloads_per_key=0 if kidx is not None else args.ppk,
                               stream=s.cuda_stream)
             e[1].record(s)
+            flush(args, torch, e, s)
+            if args.sync_between:
+                torch.cuda.synchronize()
             c.decrypt_uniform(ct, rt, n, pb, key_idx=kidx, payloads_per_key=0 if kidx is not None else args.ppk,
                               stream=s.cuda_stream)
             e[2].record(s)
@@ -89,7 +97,7 @@ def main():
                 continue
             probe(c, probes.setdefault(path, []))
             times[path]["enc"].append(e[0].elapsed_time(e[1]))
-            times[path]["dec"].append(e[1].elapsed_time(e[2]))
+            times[path]["dec"].append((e[3] if len(e) > 3 else e[1]).elapsed_time(e[2]))
     ref = digests[args.libs[0]]
     for path in args.libs:
         t = times[path]
@@ -101,6 +109,20 @@ def main():
             if waves:
                 print("    %s clock %.3f GHz, mean wave %.3f ms, max wave %.3f ms (per launch)" % (
                     kind, cyc / tick * 0.1, tick / waves / 1e5, tmax / len(v) / 1e5))
+
+
+_scratch = []
+
+
+def flush(args, torch, e, s):
+    """--flush-between: evict the caches between the launches; the decrypt is then timed from e[3]."""
+    if not args.flush_between:
+        return
+    if not _scratch:
+        _scratch.append(torch.empty(1 << 30, dtype=torch.uint8, device="cuda"))
+    _scratch[0].fill_(0x3C)
+    e.append(torch.cuda.Event(enable_timing=True))
+    e[-1].record(s)
 
 
 def relay(args, ctxs, pt, torch, s):
@@ -123,8 +145,10 @@ def relay(args, ctxs, pt, torch, s):
             else:
                 c.encrypt_ragged(buf, buf, d_off, d_nb, n, stream=s.cuda_stream)
             e[1].record(s)
-            if r == 0:
+            flush(args, torch, e, s)
+            if r == 0 or args.sync_between:
                 torch.cuda.synchronize()
+            if r == 0:
                 dct = c.digest(buf, n * stride)
             if args.relay_api == "strided":
                 c.decrypt_strided(buf, buf, hdr, stride, n, pb, stream=s.cuda_stream)
@@ -137,7 +161,7 @@ def relay(args, ctxs, pt, torch, s):
                 digests[path] = (dct, ok)
                 continue
             times[path]["enc"].append(e[0].elapsed_time(e[1]))
-            times[path]["dec"].append(e[1].elapsed_time(e[2]))
+            times[path]["dec"].append((e[3] if len(e) > 3 else e[1]).elapsed_time(e[2]))
     ref = digests[args.libs[0]][0]
     for path in args.libs:
         t = times[path]

@@ -10,7 +10,7 @@ times, and the spread inside workgroups.  The question it answers: is a
 launch's tail the waves of a few slow CUs / XCDs (a dynamic work split helps)
 or uniform (it does not).
 
-usage: python tools/timeline.py [--config B|C|D|relay] [--lib build/variants/clockprobe.so]
+usage: python tools/timeline.py [--config B|C|D|relay|relay_strided] [--lib build/variants/clockprobe.so]
        [--reps 3] [--duplex] [ENV=VALUE ...]   (context settings, e.g. CYAES_DEC_DYN=0)
 --duplex: one duplex launch (cyaes_gpu_duplex_uniform: the config's encrypt and,
 in the same grid, the decrypt of its ciphertext) instead of the two launches;
@@ -92,7 +92,7 @@ def report(name, recs, t0=None):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="B", choices=["B", "C", "D", "relay"])
+    ap.add_argument("--config", default="B", choices=["B", "C", "D", "relay", "relay_strided"])
     ap.add_argument("--lib", default=os.path.join(ROOT, "build", "variants", "clockprobe.so"))
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--duplex", action="store_true")
@@ -108,15 +108,19 @@ def main():
     lib.cyaes_debug_timeline.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     c = ca.GpuContext(0, lib=lib)
     n, pb, ppk = {"B": (1 << 20, 1472, 0), "C": (1 << 18, 65536, 0), "D": (1 << 20, 1472, 256),
-                  "relay": (1 << 20, 1472, 0)}[args.config]
+                  "relay": (1 << 20, 1472, 0), "relay_strided": (1 << 20, 1472, 0)}[args.config]
     c.set_keys(bench.session_keys(n // ppk) if ppk else bytes(range(16)))
     s = torch.cuda.current_stream().cuda_stream
     pt = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
     c.fill_synthetic(pt, 0, n, pb, 0x5EEDC1C1)
-    if args.config == "relay":
+    if args.config.startswith("relay"):  # relay packets in place: payload at 12 + p * 1,484
         hdr, stride = 12, pb + 12
         buf = torch.full((n * stride + 16,), 0xA5, dtype=torch.uint8, device="cuda")
         buf[: n * stride].view(n, stride)[:, hdr:hdr + pb] = pt.view(n, pb)
+    if args.config == "relay_strided":
+        enc = lambda: c.encrypt_strided(buf, buf, hdr, stride, n, pb, stream=s)
+        dec = lambda: c.decrypt_strided(buf, buf, hdr, stride, n, pb, stream=s)
+    elif args.config == "relay":
         off = torch.arange(n, dtype=torch.int64, device="cuda") * stride + hdr
         nb = torch.full((n,), pb, dtype=torch.int32, device="cuda")
         enc = lambda: c.encrypt_ragged(buf, buf, off, nb, n, stream=s)
