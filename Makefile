@@ -31,8 +31,11 @@ KSRC     := cyclone_amd/csrc/cyaes_kernels.hip
 ESRC     := cyclone_amd/csrc/cyaes_enc_kernels.hip
 DSRC     := cyclone_amd/csrc/cyaes_dec_kernels.hip
 XSRC     := cyclone_amd/csrc/cyaes_duplex_kernels.hip
+RSRC     := cyclone_amd/csrc/cyaes_ragged_kernels.hip
 SCHED_ENC:= -mllvm -amdgpu-sched-strategy=iterative-ilp
 SCHED_DEC:= -mllvm -amdgpu-sched-strategy=max-ilp
+SCHED_K  ?=
+SCHED_RAG?= -mllvm -amdgpu-sched-strategy=iterative-ilp
 ASRC     := cyclone_amd/csrc/cyaes_adler.hip
 BSRC     := cyclone_amd/csrc/cyaes_batch_kernels.hip
 HSRC     := cyclone_amd/csrc/cyaes_runtime.cpp cyclone_amd/csrc/cyaes_pins.cpp cyclone_amd/csrc/cyaes_tables.cpp cyclone_amd/csrc/cyr_rijndael.cpp \
@@ -42,7 +45,8 @@ HDRS     := include/cyaes.h include/cyaes_relay.h include/cyaes_batch.h include/
 KHDRS    := $(HDRS) cyclone_amd/csrc/cyaes_device.h cyclone_amd/csrc/cyaes_enc_body.h cyclone_amd/csrc/cyaes_dec_body.h \
             cyclone_amd/csrc/cyaes_lines_body.h
 
-KOBJ     := $(BUILD)/cyaes_kernels.o $(BUILD)/cyaes_enc_kernels.o $(BUILD)/cyaes_dec_kernels.o $(BUILD)/cyaes_duplex_kernels.o
+KOBJ     := $(BUILD)/cyaes_kernels.o $(BUILD)/cyaes_enc_kernels.o $(BUILD)/cyaes_dec_kernels.o $(BUILD)/cyaes_duplex_kernels.o \
+            $(BUILD)/cyaes_ragged_kernels.o
 AOBJ     := $(BUILD)/cyaes_adler.o
 BOBJ     := $(BUILD)/cyaes_batch_kernels.o
 HOBJ     := $(patsubst cyclone_amd/csrc/%.cpp,$(BUILD)/%.o,$(HSRC))
@@ -60,7 +64,7 @@ $(BUILD):
 	mkdir -p $(BUILD)
 
 $(BUILD)/cyaes_kernels.o: $(KSRC) $(KHDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(SCHED_K) -c $< -o $@
 
 $(BUILD)/cyaes_enc_kernels.o: $(ESRC) $(KHDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $(SCHED_ENC) -c $< -o $@
@@ -77,15 +81,21 @@ SCHED_DUPLEX ?= $(SCHED_ENC)
 $(BUILD)/cyaes_duplex_kernels.o: $(XSRC) $(KHDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $(SCHED_DUPLEX) -c $< -o $@
 
-# The three kernel objects of a variant build: $(call kvariant,NAME,DEFS)
+# The ragged decrypt (r05): iterative ILP (profiles/r05/ab_ragged_sched.txt)
+$(BUILD)/cyaes_ragged_kernels.o: $(RSRC) $(KHDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(SCHED_RAG) -c $< -o $@
+
+# The kernel objects of a variant build: $(call kvariant,NAME,DEFS)
 define kvariant
 	mkdir -p $(BUILD)/variants
-	$(HIPCC) $(HIPFLAGS) $(2) -c $(KSRC) -o $(BUILD)/variants/$(1).o
+	$(HIPCC) $(HIPFLAGS) $(SCHED_K) $(2) -c $(KSRC) -o $(BUILD)/variants/$(1).o
 	$(HIPCC) $(HIPFLAGS) $(SCHED_ENC) $(2) -c $(ESRC) -o $(BUILD)/variants/$(1)_enc.o
 	$(HIPCC) $(HIPFLAGS) $(SCHED_DEC) $(2) -c $(DSRC) -o $(BUILD)/variants/$(1)_dec.o
 	$(HIPCC) $(HIPFLAGS) $(SCHED_DUPLEX) $(2) -c $(XSRC) -o $(BUILD)/variants/$(1)_dup.o
+	$(HIPCC) $(HIPFLAGS) $(SCHED_RAG) $(2) -c $(RSRC) -o $(BUILD)/variants/$(1)_rag.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/$(1).so $(BUILD)/variants/$(1).o \
-	  $(BUILD)/variants/$(1)_enc.o $(BUILD)/variants/$(1)_dec.o $(BUILD)/variants/$(1)_dup.o $(AOBJ) $(BOBJ) $(HOBJ)
+	  $(BUILD)/variants/$(1)_enc.o $(BUILD)/variants/$(1)_dec.o $(BUILD)/variants/$(1)_dup.o $(BUILD)/variants/$(1)_rag.o \
+	  $(AOBJ) $(BOBJ) $(HOBJ)
 endef
 
 $(AOBJ): $(ASRC) include/cyaes_adler32.h | $(BUILD)
@@ -129,10 +139,10 @@ $(BUILD)/hostlink: tools/hostlink.hip | $(BUILD)
 $(BUILD)/microbench: tools/microbench.hip | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
-$(PROBE): $(KSRC) $(ESRC) $(DSRC) $(XSRC) $(KHDRS) $(HOBJ) $(AOBJ) $(BOBJ)
+$(PROBE): $(KSRC) $(ESRC) $(DSRC) $(XSRC) $(RSRC) $(KHDRS) $(HOBJ) $(AOBJ) $(BOBJ)
 	$(call kvariant,clockprobe,-DCYAES_CLOCK_PROBE=1)
 
-$(BOUNDS): $(KSRC) $(ESRC) $(DSRC) $(XSRC) $(KHDRS) $(HOBJ) $(AOBJ) $(BOBJ)
+$(BOUNDS): $(KSRC) $(ESRC) $(DSRC) $(XSRC) $(RSRC) $(KHDRS) $(HOBJ) $(AOBJ) $(BOBJ)
 	$(call kvariant,bounds,-DCYAES_BOUNDS_CHECK=1)
 
 # A/B variants: make variant NAME=x DEFS="-DFOO=1" -> build/variants/x.so

@@ -187,12 +187,15 @@ hipError_t launch_digest(const uint8_t* buf, uint64_t nwords, unsigned long long
 int bounds_read_enc(unsigned long long* rec4, unsigned int* lines);
 int bounds_read_dec(unsigned long long* rec4, unsigned int* lines);
 int bounds_read_dup(unsigned long long* rec4, unsigned int* lines);
+int bounds_read_rag(unsigned long long* rec4, unsigned int* lines);
 int probe_read_enc(unsigned long long* out8);
 int probe_read_dec(unsigned long long* out8);
 int probe_read_dup(unsigned long long* out8);
+int probe_read_rag(unsigned long long* out8);
 int timeline_read_dup(int kind, uint4* out);
 int timeline_read_enc(int kind, uint4* out);
 int timeline_read_dec(int kind, uint4* out);
+int timeline_read_rag(int kind, uint4* out);
 
 // Batching adapter request descriptor (cyaes_batcher.cpp builds them in pinned
 // memory, cyaes_batch_kernels.hip reads them).  src / dst are DEVICE

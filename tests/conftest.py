@@ -5,6 +5,16 @@ import sys
 
 import pytest
 
+# The HIP runtime pins a pageable source of more than GPU_PINNED_MIN_XFER_SIZE
+# MiB (1 here) on the fly for a host-to-device copy.  Twice in r04 and once in
+# r05 such a torch copy of a fresh numpy array faulted with
+# hipErrorIllegalAddress at the start of a test, with no kernel of the library
+# in flight and, in r05, no registration of the library live (cyaes_debug_pins
+# checked after every test): a stale pin of that runtime path, not of this
+# library.  The test harness's own copies therefore go through
+# the runtime's staging buffer at every size.
+os.environ.setdefault("GPU_PINNED_MIN_XFER_SIZE", str(1 << 20))
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))

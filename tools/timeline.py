@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 WAVES = 8192
 
 
-def records(lib, kind, tus=(0, 1, 2)):
+def records(lib, kind, tus=(0, 1, 2, 4)):
     """Timeline records of the last launch of `kind` (0 enc, 1 dec) from whichever kernel TU ran it."""
     out = []
     for tu in tus:
