@@ -290,6 +290,75 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
     return make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));  // next carry
 }
 
+// In-place launches with static ranges hand each range's carry C[begin-1]
+// over without a prepass (DecArgs.handoff = the launch's epoch, unique in the
+// process; boundary = one 32-B record per range: the block, then the epoch).
+// Before its first store, a wave publishes for each of its ranges t the last
+// ciphertext block C[end-1] -- still ciphertext: only this wave writes it --
+// into record t+1, then the epoch, each behind an agent-scope release fence,
+// so the epoch is visible before any plaintext of the range.  Then, for each
+// of its ranges that starts inside a payload, it loads C[begin-1] from the
+// stream and (acquire) the record's epoch: published, the record holds the
+// block; not published, range t-1's wave has not stored anything yet, so the
+// loaded block is ciphertext and the wave writes it into the record itself
+// (a writer arriving later writes the same bytes).  Neither side waits for the
+// other, so nothing assumes the waves are resident together.  The range loop
+// then reads its carry from the record, as from the prepass's snapshot.
+template <bool STRIDED>
+__device__ __forceinline__ uint4 dec_blk_at(const DecArgs& a, const uint8_t* in, uint64_t nblocks, uint64_t g) {
+    if (STRIDED) return LD16U(a.in + soff_g(a, g), data_ext(a.in, a, true));
+    return LD16(in + 16 * g, ext(in, 16 * nblocks));
+}
+// The records are written and read with agent-scope relaxed atomics (coherent
+// across the XCDs' L2s without writing back or invalidating them), ordered by
+// waits for the wave's own memory accesses to complete (vm_drain; the
+// workgroup-scope fence emits none between two stores): an agent-scope fence
+// here writes back and invalidates the whole L2 at every wave's start
+// (measured +5 % on a relay-sized in-place decrypt).
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // s_waitcnt vmcnt(0) (gfx9 encoding)
+__device__ __forceinline__ void rec_store(uint4* r, uint4 v) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(r);
+    __hip_atomic_store(w + 0, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(w + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(w + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(w + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint4 rec_load(const uint4* r) {
+    uint32_t* w = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(r));
+    return make_uint4(__hip_atomic_load(w + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                      __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                      __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                      __hip_atomic_load(w + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+template <bool STRIDED>
+__device__ __forceinline__ void dec_handoff(const DecArgs& a, uint64_t wave, uint64_t nwaves, uint32_t lane) {
+    uint4* rec = const_cast<uint4*>(a.boundary);
+    const uint64_t nblocks = a.nblocks, epoch = a.handoff, len = a.stat_blocks;
+    const uint32_t bpp = a.bpp.d;
+    const Ext re = ext(rec, 32ull * a.nranges);
+    for (uint64_t t = wave; t < a.nstat; t += nwaves) {
+        const uint64_t end = min((t + 1) * len, nblocks);
+        if (end >= nblocks || end % bpp == 0) continue;  // range t + 1 starts a payload (or does not exist)
+        const uint4 last = dec_blk_at<STRIDED>(a, a.in, nblocks, end - 1);
+        if (lane == 0) rec_store(AT(rec + 2 * (t + 1), re, 16), last);
+        vm_drain();  // the block before the epoch
+        if (lane == 0)
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(AT(rec + 2 * (t + 1) + 1, re, 8)), epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        vm_drain();  // the epoch before any plaintext store
+    }
+    for (uint64_t t = wave; t < a.nstat; t += nwaves) {
+        const uint64_t begin = t * len;
+        if (begin == 0 || begin % bpp == 0) continue;  // starts a payload: no carry
+        const uint4 prev = dec_blk_at<STRIDED>(a, a.in, nblocks, begin - 1);
+        vm_drain();  // the block loaded before the epoch is
+        const uint64_t e = __hip_atomic_load(reinterpret_cast<uint64_t*>(AT(rec + 2 * t + 1, re, 8)), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        if (e != epoch && lane == 0) rec_store(AT(rec + 2 * t, re, 16), prev);
+    }
+    vm_drain();  // the records as the range loop will read them
+}
+
 // SESS: sessions of payloads_per_key payloads that are whole steps long
 // (a.sess_blocks, a multiple of 64 * R; config D: 256 x 92 blocks) and whole
 // ranges long: no range straddles two sessions, so the unkeyed step runs under
@@ -326,6 +395,7 @@ __device__ __forceinline__ void dec_flat_body(const DecArgs& a, const char* lds,
     // runtime launches them (the range loop around their larger step bodies
     // cost VGPR spills).
     const uint32_t nwaves = gridDim.x * (kDecThreads / 64);
+    if (a.handoff) dec_handoff<STRIDED>(a, wave, nwaves, lane);
     uint32_t pool = xcc_id();
     uint32_t ticket = (uint32_t)wave;
     if (a.dyn && ticket >= a.nstat)
@@ -350,7 +420,8 @@ __device__ __forceinline__ void dec_flat_body(const DecArgs& a, const char* lds,
         ps.bpos = (uint32_t)(begin - ps.bp * a.bpp.d);
         uint4 carry = make_uint4(0, 0, 0, 0);  // C[begin-1]
         if (ps.bpos != 0) {  // (begin >= 1 here)
-            if (ka->boundary) carry = LD16(ka->boundary + ticket, ext(ka->boundary, 16ull * ka->nranges));
+            if (ka->boundary && ka->handoff) carry = rec_load(AT(ka->boundary + 2 * ticket, ext(ka->boundary, 32ull * ka->nranges), 16));
+            else if (ka->boundary) carry = LD16(ka->boundary + 2 * ticket, ext(ka->boundary, 32ull * ka->nranges));
             else if (STRIDED) carry = LD16U(a.in + soff(a, ps.bp, ps.bpos - 1), data_ext(a.in, a, true));
             else carry = LD16(ka->in + 16 * (begin - 1), ext(ka->in, 16 * ka->nblocks));
         }

@@ -30,8 +30,8 @@ __global__ void k_dec_prepass(DecArgs a, uint32_t work_words) {
     if (!a.boundary || r >= a.nranges) return;
     const uint64_t begin = r < a.nstat ? r * a.stat_blocks : a.nstat * a.stat_blocks + (r - a.nstat) * a.range_blocks;
     if (begin == 0 || begin >= a.nblocks || begin % a.bpp.d == 0) return;
-    uint4* snap = const_cast<uint4*>(a.boundary) + r;
-    const Ext se = ext(a.boundary, 16 * a.nranges);
+    uint4* snap = const_cast<uint4*>(a.boundary) + 2 * r;  // (32-B records: dec_handoff's layout)
+    const Ext se = ext(a.boundary, 32 * a.nranges);
     if (a.stride) ST16(snap, se, LD16U(a.in + soff_g(a, begin - 1), data_ext(a.in, a, true)));
     else ST16(snap, se, LD16(a.in + 16 * (begin - 1), ext(a.in, 16 * a.nblocks)));
 }

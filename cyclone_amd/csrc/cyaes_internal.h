@@ -144,13 +144,17 @@ struct DecArgs {
     KeySel keys;
     const uint8_t* iv_in;
     uint8_t* iv_out;
-    const uint4* boundary;    // flat kernel in-place: C[begin-1] per range (nullable)
+    const uint4* boundary;    // flat kernel in-place: a 32-B record per range, C[begin-1] first (nullable)
     uint32_t inplace;         // in == out: drain a step's loads before its stores
     const uint32_t* tables;   // kDecTableWords
     uint32_t* status;
     uint32_t group;           // ragged kernel: payloads per wave group (1..64)
     uint64_t sess_blocks;     // flat kernel: blocks per payloads_per_key session when a multiple of a step, else 0
     uint64_t off0, stride;    // flat kernel, stride != 0: payload p at byte off0 + p * stride (4-B aligned), else contiguous
+    // Flat kernel in place, static ranges, no prepass: != 0 the launch's epoch,
+    // with which the waves tag the boundary records they publish (dec_handoff,
+    // cyaes_dec_body.h).
+    uint64_t handoff;
 };
 
 // The duplex launch (cyaes_duplex_kernels.hip): one grid encrypts batch e,

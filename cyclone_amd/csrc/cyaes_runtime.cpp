@@ -33,6 +33,7 @@ struct cyaes_gpu {
     int dec_grid_max = 0;       // env CYAES_DEC_GRID: cap on decrypt workgroups (tests: many ranges per wave on small batches)
     bool strided_lists = false; // env CYAES_STRIDED_LISTS=1: strided decrypts as ragged batches (tests, A/B)
     bool strided_force = false; // env CYAES_STRIDED_FORCE=1: contiguous strided batches keep the strided kernels (A/B)
+    bool dec_handoff = true;    // env CYAES_DEC_HANDOFF=0: in-place static decrypts snapshot their carries in a prepass
     bool duplex_off = false;    // env CYAES_DUPLEX=0: duplex calls run as two launches (tests, A/B)
     uint32_t duplex_dyn_pct = kDuplexDynPct;  // env CYAES_DUPLEX_DYN_PCT: the duplex decrypt's pool share (%)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
@@ -501,14 +502,22 @@ int dec_plan(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t npayloads
     if (st) return st;
     a.work = static_cast<uint32_t*>(work.p);
     if (in == out && a.nranges > 1) {
-        st = boundary.get(ctx, a.nranges * sizeof(uint4), stream);
+        // A 32-B record per range.  Static ranges hand their carries over in the
+        // kernel (records tagged with this launch's epoch: dec_handoff); dynamic
+        // ones, whose ticket counters need the prepass anyway, have it snapshot them.
+        const bool handoff = !a.dyn && ctx->dec_handoff;
+        st = boundary.get(ctx, a.nranges * 2 * sizeof(uint4), stream);
         if (st) return st;
         a.boundary = static_cast<uint4*>(boundary.p);
+        if (handoff) {
+            static std::atomic<uint64_t> epochs{0};
+            a.handoff = ++epochs;  // unique in the process: a recycled scratch block's old records never match
+        }
     }
     // The ticket counter (dyn) and the boundary snapshot need the prepass; the
     // progress words are reset by their workgroups.  A small static batch (the
     // drop-in's packet) launches the kernel alone, as before.
-    if (a.dyn || a.boundary) CY_TRY(launch_dec_prepass(a, ww, stream));
+    if (a.dyn || (a.boundary && !a.handoff)) CY_TRY(launch_dec_prepass(a, ww, stream));
     return CYAES_OK;
 }
 
@@ -658,6 +667,7 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* v = getenv("CYAES_DEC_DYN_PCT")) ctx->dec_dyn_pct = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_STRIDED_LISTS")) ctx->strided_lists = atoi(v) != 0;
     if (const char* v = getenv("CYAES_STRIDED_FORCE")) ctx->strided_force = atoi(v) != 0;
+    if (const char* v = getenv("CYAES_DEC_HANDOFF")) ctx->dec_handoff = atoi(v) != 0;
     if (const char* v = getenv("CYAES_DUPLEX")) ctx->duplex_off = atoi(v) == 0;
     if (const char* v = getenv("CYAES_DUPLEX_DYN_PCT")) ctx->duplex_dyn_pct = (uint32_t)strtoul(v, nullptr, 10);
     const HostTables& t = host_tables();

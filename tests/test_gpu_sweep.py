@@ -167,3 +167,39 @@ def test_batch_sweep(torch, seed):
         assert c.check() == ca.CYAES_OK
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("layout", ["uniform", "strided"])
+@pytest.mark.parametrize("grid", [None, "1", "2", "5"])
+@pytest.mark.parametrize("handoff", [None, "0"])
+def test_inplace_decrypt_range_handoff(torch, layout, grid, handoff):
+    """In-place flat decrypts whose static ranges start inside payloads: the
+    carries handed over in the kernel (DecArgs.handoff, the default) or
+    snapshot by the prepass (CYAES_DEC_HANDOFF=0), on full and small grids,
+    against the oracle (cyr_rijndael.cpp:612-635 per payload)."""
+    rng = np.random.default_rng(77 + (grid is not None) * int(grid or 0) + (layout == "strided") * 10)
+    n, bpp = 301, 92  # 27,692 blocks: ranges end inside payloads on every grid here
+    pb = 16 * bpp
+    key = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+    stride, first = (pb + 12, 12) if layout == "strided" else (pb, 0)
+    plain = rng.integers(0, 256, first + n * stride + 64, dtype=np.uint8)
+    ct = plain.copy()
+    r = oracle.Rijndael(key)
+    for p in range(n):
+        o = first + p * stride
+        ct[o:o + pb] = np.frombuffer(bytes(r.encrypt(plain[o:o + pb].tobytes(), None, pb,
+                                                     bytearray(oracle.default_iv()))), np.uint8)
+    c = context({"CYAES_DEC_GRID": grid, "CYAES_DEC_DYN": "0", "CYAES_DEC_HANDOFF": handoff})
+    try:
+        c.set_keys(key)
+        d = dev(torch, ct)
+        for _ in range(3):  # repeated launches: every one tags its records with a new epoch
+            d.copy_(dev(torch, ct))
+            if layout == "strided":
+                c.decrypt_strided(d, d, first, stride, n, pb)
+            else:
+                c.decrypt_uniform(d, d, n, pb)
+            assert np.array_equal(host(d), plain)
+        assert c.check() == ca.CYAES_OK
+    finally:
+        c.close()
