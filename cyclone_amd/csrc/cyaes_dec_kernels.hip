@@ -49,8 +49,7 @@ static void launch_flat(const DecArgs& a, dim3 g, dim3 b, hipStream_t stream) {
     else if (a.stride) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false, true, DIV>), g, b, 0, stream, a);
     else if (sess && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, true, false, false, DIV>), g, b, 0, stream, a);
     else if (sess) hipLaunchKernelGGL((k_decrypt_flat<false, false, true, false, false, DIV>), g, b, 0, stream, a);
-    else if (keyed && big) hipLaunchKernelGGL((k_decrypt_flat<true, true, false, true, false, kDecPrioDiv>), g, b, 0, stream, a);
-    else if (keyed) hipLaunchKernelGGL((k_decrypt_flat<true, false, false, true, false, kDecPrioDiv>), g, b, 0, stream, a);
+    else if (keyed) launch_decrypt_flat_keyed(a, g, b, stream);  // (cyaes_ragged_kernels.hip: iterative ILP)
     else if (big && iv) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, true, false, kDecPrioDiv>), g, b, 0, stream, a);
     else if (big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false, false, DIV>), g, b, 0, stream, a);
     else if (iv) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, true, false, kDecPrioDiv>), g, b, 0, stream, a);

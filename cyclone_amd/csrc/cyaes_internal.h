@@ -174,6 +174,8 @@ hipError_t launch_encrypt_lines(const EncArgs& a, int grid, int threads, hipStre
 hipError_t launch_encrypt_quad(const EncArgs& a, int grid, int threads, hipStream_t stream);
 hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream);
 hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, int threads, hipStream_t stream);
+// The flat decrypt's per-payload-key instantiations (cyaes_ragged_kernels.hip): for launch_decrypt_flat.
+void launch_decrypt_flat_keyed(const DecArgs& a, dim3 g, dim3 b, hipStream_t stream);
 hipError_t launch_duplex(const DuplexArgs& x, int grid, hipStream_t stream);  // 1024-thread workgroups
 // Before a decrypt: zeroes its work words and, for an in-place flat decrypt
 // (boundary != NULL), snapshots C[begin-1] of every range that starts inside a payload.

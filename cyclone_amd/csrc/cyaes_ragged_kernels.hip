@@ -1,6 +1,7 @@
 // cyaes_ragged_kernels.hip -- gfx950 CBC decrypt of ragged batches
 // (k_decrypt_ragged; cyr_rijndael.cpp:612-635 + _decryptBlock :708-774): the
-// payloads of a device offset / size list, in groups packed into wave rows.
+// payloads of a device offset / size list, in groups packed into wave rows;
+// and the flat decrypt's per-payload-key instantiations (k_decrypt_flat_keyed).
 // Its own translation unit since r05, compiled with the iterative ILP scheduler
 // (Makefile SCHED_RAG): under the default scheduler of cyaes_kernels.hip the
 // step issued its LDS reads 4-8 at a time; moved here with a scheduling
@@ -8,7 +9,7 @@
 // entry points takes -2.8 % (profiles/r05/ab_ragged_sched.txt), while the quad
 // encrypt left in cyaes_kernels.hip measured +4 % under this scheduler.
 #define CYAES_TU 4
-#include "cyaes_device.h"
+#include "cyaes_dec_body.h"
 
 namespace cyaes {
 namespace {
@@ -254,7 +255,30 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     }
 }
 
+// The flat decrypt with per-payload keys (key index arrays, sessions that are
+// not whole steps; with IV arrays): under the decrypt unit's max-ILP scheduler
+// its step issued the LDS reads 4-7 at a time (320 s_waitcnt per 640 reads),
+// here in bursts of 64 (13): config D's sessions given as a key index array
+// decrypt -8.5 % (profiles/r05/ab_dec_keyed_sched.txt).  The other flat
+// instantiations stay in cyaes_dec_kernels.hip, where the strided one keeps
+// its registers (6 VGPR spills under this scheduler, +1 %).
+template <bool BIG>
+__global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat_keyed(DecArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
+    fill_dec_image(lds_words, a.tables);
+    uint32_t* leadp = dec_lead_word(a.work);
+    if (threadIdx.x == 0) *leadp = 0;
+    __syncthreads();
+    CLOCK_PROBE(1);
+    dec_flat_body<true, BIG, false, true, false, kDecPrioDiv, 0>(a, reinterpret_cast<const char*>(lds_words), leadp);
+}
+
 }  // namespace
+
+void launch_decrypt_flat_keyed(const DecArgs& a, dim3 g, dim3 b, hipStream_t stream) {
+    if (a.bpp.d >= 64u * kDecRows) hipLaunchKernelGGL(k_decrypt_flat_keyed<true>, g, b, 0, stream, a);
+    else hipLaunchKernelGGL(k_decrypt_flat_keyed<false>, g, b, 0, stream, a);
+}
 
 hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, int threads, hipStream_t stream) {
     const bool keyed = a.keys.key_idx != nullptr || a.keys.ppk.d != 0;
