@@ -203,3 +203,37 @@ def test_inplace_decrypt_range_handoff(torch, layout, grid, handoff):
         assert c.check() == ca.CYAES_OK
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("pb", [1040, 1472, 4096])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_strided_kernels_on_contiguous_payloads(torch, pb, inplace):
+    """CYAES_STRIDED_FORCE=1 keeps the strided kernels (k_encrypt_lines / the
+    flat decrypt's STRIDED rows) on payloads that are back to back, which the
+    runtime otherwise hands to the uniform kernels: the A/B that located the
+    strided decrypt's cost in its code, not its layout.
+    Against the oracle, both directions."""
+    rng = np.random.default_rng(pb + inplace)
+    n, first = 2048 + 37, 64
+    key = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+    plain = rng.integers(0, 256, first + n * pb + 64, dtype=np.uint8)
+    ct = plain.copy()
+    r = oracle.Rijndael(key)
+    for p in range(n):
+        o = first + p * pb
+        ct[o:o + pb] = np.frombuffer(bytes(r.encrypt(plain[o:o + pb].tobytes(), None, pb,
+                                                     bytearray(oracle.default_iv()))), np.uint8)
+    c = context({"CYAES_STRIDED_FORCE": "1"})
+    try:
+        c.set_keys(key)
+        src = dev(torch, plain)
+        dst = src if inplace else dev(torch, plain)
+        c.encrypt_strided(src, dst, first, pb, n, pb)
+        assert np.array_equal(host(dst), ct)
+        src = dev(torch, ct)
+        dst = src if inplace else dev(torch, ct)
+        c.decrypt_strided(src, dst, first, pb, n, pb)
+        assert np.array_equal(host(dst), plain)
+        assert c.check() == ca.CYAES_OK
+    finally:
+        c.close()
