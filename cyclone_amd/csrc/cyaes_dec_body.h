@@ -295,13 +295,14 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
 // process; boundary = one 32-B record per range: the block, then the epoch).
 // Before its first store, a wave publishes for each of its ranges t the last
 // ciphertext block C[end-1] -- still ciphertext: only this wave writes it --
-// into record t+1, then the epoch, each behind an agent-scope release fence,
-// so the epoch is visible before any plaintext of the range.  Then, for each
-// of its ranges that starts inside a payload, it loads C[begin-1] from the
-// stream and (acquire) the record's epoch: published, the record holds the
-// block; not published, range t-1's wave has not stored anything yet, so the
-// loaded block is ciphertext and the wave writes it into the record itself
-// (a writer arriving later writes the same bytes).  Neither side waits for the
+// into record t+1, then the epoch, each store completed before the next
+// access, so the epoch is visible before any plaintext of the range.  Then,
+// for each of its ranges that starts inside a payload, it loads C[begin-1]
+// from the stream and, once that load has completed, the record's epoch:
+// published, the record holds the block; not published, range t-1's wave has
+// not stored anything yet, so the loaded block is ciphertext and the wave
+// writes it into the record itself (a writer arriving later writes the same
+// bytes).  Neither side waits for the
 // other, so nothing assumes the waves are resident together.  The range loop
 // then reads its carry from the record, as from the prepass's snapshot.
 template <bool STRIDED>
