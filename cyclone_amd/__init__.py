@@ -93,6 +93,8 @@ _SIGS = {
     "cyaes_gpu_cbc_encrypt_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "cyaes_gpu_cbc_decrypt_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "cyaes_debug_pins": (ctypes.c_int, [_u64p]),
+    "cyaes_debug_ctx": (ctypes.c_int, [_vp, _u64p]),
+    "cyaes_debug_pin_history": (ctypes.c_uint64, [_u64p, ctypes.c_uint64, _u64p]),
     "cyaes_gpu_duplex_uniform": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                                 _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     # include/cyaes_relay.h
@@ -192,6 +194,16 @@ def debug_pins():
     out = (ctypes.c_uint64 * 8)()
     _check(load_library().cyaes_debug_pins(out), "cyaes_debug_pins")
     return dict(zip(PIN_FIELDS, (int(v) for v in out)))
+
+
+def debug_pin_history(cap=1024):
+    """(ranges, outlived): the [lo, hi) host ranges the library unregistered,
+    most recent first, and how many unregisters found their memory already
+    unmapped (cyaes_debug_pin_history, include/cyaes.h)."""
+    out = (ctypes.c_uint64 * (2 * cap))()
+    outlived = ctypes.c_uint64(0)
+    n = load_library().cyaes_debug_pin_history(out, cap, ctypes.byref(outlived))
+    return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)], int(outlived.value)
 
 
 def key_expand(key):
@@ -333,6 +345,12 @@ class GpuContext:
             raise ValueError("keys must be a non-empty multiple of 16 bytes")
         buf = (ctypes.c_uint8 * len(keys)).from_buffer_copy(keys)
         _check(self._lib.cyaes_gpu_update_keys(self._h, first, ctypes.addressof(buf), len(keys) // 16), "update_keys")
+
+    def debug_state(self):
+        """cyaes_debug_ctx: key-table readers in flight, scratch blocks / bytes, outgrown tables."""
+        out = (ctypes.c_uint64 * 4)()
+        _check(self._lib.cyaes_debug_ctx(self._h, out), "cyaes_debug_ctx")
+        return dict(zip(("key_uses", "scratch_blocks", "scratch_bytes", "retired_tables"), (int(v) for v in out)))
 
     def set_keys_device(self, d_keys, nkeys, stream=None):
         _check(self._lib.cyaes_gpu_set_keys_device(self._h, _p(d_keys), nkeys, _p(stream)), "set_keys_device")

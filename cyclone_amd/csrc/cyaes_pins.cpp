@@ -19,8 +19,11 @@
 // several batchers on one page) instead of registered twice, and every
 // unregister's status checked and counted.  cyaes_debug_pins() reports the counters; tests/conftest.py asserts
 // after every GPU test that nothing the library registered is still live.
+#include <errno.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
+#include <deque>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -46,7 +49,14 @@ struct Registry {
     std::map<uintptr_t, Reg> regs;  // by first page
     uint64_t live_bytes = 0;
     uint64_t registered = 0, unregistered = 0, failed_unregisters = 0, stale = 0, foreign_conflicts = 0;
+    // r06: the byte ranges released, most recent first,
+    // for the test harness's after-test check that the runtime answers for
+    // none of them any more; and the unregisters that found some of the
+    // range's pages already unmapped (a registration that outlived its memory).
+    std::deque<std::pair<uintptr_t, uintptr_t>> released;
+    uint64_t outlived = 0;
 };
+constexpr size_t kReleasedKept = 1024;
 
 Registry& reg() {
     static Registry r;
@@ -93,6 +103,10 @@ bool inside_one_foreign(uintptr_t lo, uintptr_t hi) {
 // Unregisters one library registration (mu held) and checks that the runtime
 // no longer answers for its first and last byte.
 int unregister_one(Registry& r, const Reg& g) {
+    // Still mapped?  msync fails with ENOMEM when a page of the range is not
+    // (a query: nothing is written back for anonymous memory).
+    const uintptr_t plo = page_down(g.lo);
+    if (msync(reinterpret_cast<void*>(plo), page_up(g.hi) - plo, MS_ASYNC) != 0 && errno == ENOMEM) r.outlived++;
     const hipError_t e = hipHostUnregister(reinterpret_cast<void*>(g.lo));
     int st = CYAES_OK;
     if (e != hipSuccess) {
@@ -113,6 +127,8 @@ int unregister_one(Registry& r, const Reg& g) {
         }
     }
     r.live_bytes -= g.hi - g.lo;
+    r.released.push_front({g.lo, g.hi});
+    if (r.released.size() > kReleasedKept) r.released.pop_back();
     return st;
 }
 
@@ -246,4 +262,18 @@ extern "C" int cyaes_debug_pins(uint64_t out[8]) {
     for (const auto& kv : r.regs) refs += kv.second.refs;
     out[7] = refs;
     return CYAES_OK;
+}
+
+extern "C" uint64_t cyaes_debug_pin_history(uint64_t* out, uint64_t cap, uint64_t* outlived) {
+    cyaes::Registry& r = cyaes::reg();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (outlived) *outlived = r.outlived;
+    uint64_t n = 0;
+    for (const auto& x : r.released) {
+        if (!out || n == cap) break;
+        out[2 * n] = x.first;
+        out[2 * n + 1] = x.second;
+        n++;
+    }
+    return n;
 }

@@ -117,11 +117,26 @@ int make_keysel(const cyaes_gpu* ctx, uint64_t npayloads, const uint32_t* key_id
 bool reads_ctx_keys(const cyaes_gpu* ctx, const uint32_t* table) {
     return ctx->d_keys && table >= ctx->d_keys && table < ctx->d_keys + (uint64_t)ctx->key_cap * kSchedWords;
 }
+// Entries whose batches have completed are dropped on the way (r06, ADVICE
+// r05): the list holds only streams with a table reader still in flight, so a
+// caller that uses a new stream per request does not grow it, and a key write
+// waits for at most that many events.
 int note_key_use(cyaes_gpu* ctx, const uint32_t* table, hipStream_t stream) {
     if (!reads_ctx_keys(ctx, table)) return CYAES_OK;
     std::lock_guard<std::mutex> lk(ctx->key_mu);
-    for (auto& u : ctx->key_uses)
-        if (u.first == stream) return map_err(hipEventRecord(u.second, stream));
+    auto& v = ctx->key_uses;
+    for (size_t i = 0; i < v.size();) {
+        if (v[i].first == stream) return map_err(hipEventRecord(v[i].second, stream));
+        const hipError_t q = hipEventQuery(v[i].second);
+        if (q == hipSuccess) {
+            (void)hipEventDestroy(v[i].second);
+            v[i] = v.back();
+            v.pop_back();
+            continue;
+        }
+        if (q != hipErrorNotReady) return map_err(q);
+        i++;
+    }
     hipEvent_t ev = nullptr;
     CY_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     ctx->key_uses.push_back({stream, ev});
@@ -301,6 +316,41 @@ struct StreamScratch {
     size_t idx = 0;
     hipStream_t s = nullptr;
     int get(cyaes_gpu* c, uint64_t bytes, hipStream_t stream) {
+        std::vector<ScratchVictim> victims;
+        uint64_t cap = 0;
+        const int st = pick(c, bytes, stream, &victims, &cap);
+        // hipFree and hipMalloc may wait for the device: never under the
+        // mutex, so a new block is made after it is released.
+        for (const auto& x : victims) {
+            (void)hipFree(x.first);
+            (void)hipEventDestroy(x.second);
+        }
+        if (st || p) return st;
+        void* mem = nullptr;
+        hipEvent_t ev = nullptr;
+        hipError_t e = hipMalloc(&mem, cap);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        std::lock_guard<std::mutex> lk(c->scratch_mu);
+        if (e != hipSuccess) {
+            if (mem) (void)hipFree(mem);
+            c->scratch_bytes -= cap;  // (reserved by pick)
+            return map_err(e);
+        }
+        auto& v = c->scratch;
+        size_t slot = 0;  // an empty slot, else a new one
+        while (slot < v.size() && v[slot].p) slot++;
+        if (slot == v.size()) v.push_back({});
+        v[slot] = {mem, cap, ev, stream, true, false};
+        p = mem;
+        ctx = c;
+        idx = slot;
+        s = stream;
+        return CYAES_OK;
+    }
+    using ScratchVictim = std::pair<void*, hipEvent_t>;
+    // Under the mutex: hands out a cached block (p set), or reserves `cap`
+    // bytes for a new one and takes out the completed blocks trim() frees.
+    int pick(cyaes_gpu* c, uint64_t bytes, hipStream_t stream, std::vector<ScratchVictim>* victims, uint64_t* cap_out) {
         std::lock_guard<std::mutex> lk(c->scratch_mu);
         auto& v = c->scratch;
         // Preference: a completed block, or one whose last user was this very
@@ -331,21 +381,10 @@ struct StreamScratch {
         if (best == v.size()) {
             uint64_t cap = 4096;
             while (cap < bytes) cap *= 2;
-            trim(c, cap);
-            void* mem = nullptr;
-            CY_TRY(hipMalloc(&mem, cap));
-            hipEvent_t ev = nullptr;
-            const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-            if (e != hipSuccess) {
-                (void)hipFree(mem);
-                return map_err(e);
-            }
-            size_t slot = 0;  // a slot trim() emptied, else a new one
-            while (slot < v.size() && v[slot].p) slot++;
-            if (slot == v.size()) v.push_back({});
-            v[slot] = {mem, cap, ev, stream, false, false};
+            trim(c, cap, victims);
             c->scratch_bytes += cap;
-            best = slot;
+            *cap_out = cap;
+            return CYAES_OK;
         }
         v[best].in_use = true;
         p = v[best].p;
@@ -356,10 +395,10 @@ struct StreamScratch {
     }
     // Before caching `adding` more bytes: frees completed blocks, largest
     // first, while the cache would exceed kScratchCacheBytes (a large call's
-    // block is not kept for the context's life).  hipFree may wait
-    // for the device, so this runs only when a block is about to be allocated
-    // anyway and the cache is over its cap.
-    static void trim(cyaes_gpu* c, uint64_t adding) {
+    // block is not kept for the context's life).  Runs only when a
+    // block is about to be allocated anyway and the cache is over its cap; the
+    // blocks go to `victims`, freed by the caller after the mutex is released.
+    static void trim(cyaes_gpu* c, uint64_t adding, std::vector<ScratchVictim>* victims) {
         auto& v = c->scratch;
         while (c->scratch_bytes + adding > kScratchCacheBytes) {
             size_t big = v.size();
@@ -370,8 +409,7 @@ struct StreamScratch {
             }
             (void)hipGetLastError();
             if (big == v.size()) return;
-            (void)hipFree(v[big].p);
-            (void)hipEventDestroy(v[big].done);
+            victims->push_back({v[big].p, v[big].done});
             c->scratch_bytes -= v[big].bytes;
             v[big] = {};  // an empty slot: the indices held by calls in flight stay valid
         }
@@ -717,6 +755,19 @@ int cyaes_gpu_device(const cyaes_gpu* ctx) { return ctx ? ctx->device : -1; }
 int cyaes_gpu_num_cus(const cyaes_gpu* ctx) { return ctx ? ctx->num_cus : 0; }
 uint32_t cyaes_gpu_nkeys(const cyaes_gpu* ctx) { return ctx ? ctx->nkeys : 0; }
 
+int cyaes_debug_ctx(cyaes_gpu* ctx, uint64_t out[4]) {
+    if (!ctx || !out) return CYAES_EINVAL;
+    {
+        std::lock_guard<std::mutex> lk(ctx->key_mu);
+        out[0] = ctx->key_uses.size();
+        out[3] = ctx->retired_keys.size();
+    }
+    std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+    out[1] = (uint64_t)std::count_if(ctx->scratch.begin(), ctx->scratch.end(), [](const auto& b) { return b.p != nullptr; });
+    out[2] = ctx->scratch_bytes;
+    return CYAES_OK;
+}
+
 // A private non-blocking stream for one key-table copy, destroyed after it.
 // Not kept in the context: the box gives a process 4 hardware queues
 // (GPU_MAX_HW_QUEUES) and streams beyond that share them, so a context-lifetime
@@ -738,6 +789,8 @@ struct KeyStream {
 static int wait_key_readers(cyaes_gpu* ctx) {
     std::lock_guard<std::mutex> lk(ctx->key_mu);
     for (auto& u : ctx->key_uses) CY_TRY(hipEventSynchronize(u.second));
+    for (auto& u : ctx->key_uses) (void)hipEventDestroy(u.second);  // all complete: nothing left to wait for
+    ctx->key_uses.clear();
     return CYAES_OK;
 }
 static int wait_key_writes(cyaes_gpu* ctx) {
@@ -844,6 +897,10 @@ int cyaes_gpu_set_keys_device(cyaes_gpu* ctx, const uint8_t* d_keys, uint32_t nk
         for (auto& u : ctx->key_uses)
             if (u.first != s) CY_TRY(hipStreamWaitEvent(s, u.second, 0));
     }
+    // ... and for an expansion still pending from an earlier set_keys_device
+    // on another stream (r06): rows are written in call
+    // order, and keys_written, re-recorded below, then covers both.
+    if (ctx->keys_written_pending) CY_TRY(hipStreamWaitEvent(s, ctx->keys_written, 0));
     const uint8_t* d_sbox = reinterpret_cast<const uint8_t*>(ctx->d_tables) + kSboxOff;
     CY_TRY(launch_key_expand(d_keys, nkeys, d_sbox, ctx->d_keys, s));
     CY_TRY(hipEventRecord(ctx->keys_written, s));

@@ -230,6 +230,20 @@ int cyaes_gpu_digest(const uint8_t* d_buf, uint64_t nbytes, uint64_t out[2], voi
  * held.  Out[4] and out[5] are 0 unless the runtime misbehaves; out[0] is 0
  * whenever no pool is registered and no host batch runs. */
 int cyaes_debug_pins(uint64_t out[8]);
+/* The host byte ranges the library has unregistered, most recent first (up to
+ * the last 1,024): writes min(cap, kept) [lo, hi) pairs to out and returns
+ * their number.  *outlived (nullable) = unregisters that found a page of the
+ * range already unmapped, i.e. a registration that outlived its memory (the
+ * precondition of a stale registration record; 0 unless a caller freed a pool
+ * before unregistering it). */
+uint64_t cyaes_debug_pin_history(uint64_t* out, uint64_t cap, uint64_t* outlived);
+
+/* A context's bookkeeping: out[0] streams with a batch that read the key table
+ * still in flight (entries whose batches completed are dropped on the next
+ * batch or key write, so this stays bounded by the streams in use), out[1]
+ * cached scratch blocks, out[2] their bytes, out[3] outgrown key tables kept
+ * until destroy. */
+int cyaes_debug_ctx(cyaes_gpu* ctx, uint64_t out[4]);
 
 #ifdef __cplusplus
 }

@@ -5,16 +5,6 @@ import sys
 
 import pytest
 
-# The HIP runtime pins a pageable source of more than GPU_PINNED_MIN_XFER_SIZE
-# MiB (1 here) on the fly for a host-to-device copy.  Twice in r04 and once in
-# r05 such a torch copy of a fresh numpy array faulted with
-# hipErrorIllegalAddress at the start of a test, with no kernel of the library
-# in flight and, in r05, no registration of the library live (cyaes_debug_pins
-# checked after every test): a stale pin of that runtime path, not of this
-# library.  The test harness's own copies therefore go through
-# the runtime's staging buffer at every size.
-os.environ.setdefault("GPU_PINNED_MIN_XFER_SIZE", str(1 << 20))
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -61,6 +51,17 @@ def _gpu_fault_guard(request):
     pins = cyclone_amd.debug_pins()
     assert pins["live"] == 0 and pins["refs"] == 0, "library host registrations still live: %s" % pins
     assert pins["failed_unregisters"] == 0 and pins["stale"] == 0, "host unregister failed: %s" % pins
+    # Every range registered this session (the library's registry and the
+    # tests' own hipHostRegister calls, tests/hiprt.py), released or freed:
+    # the runtime answers for none of them any more, and none was unregistered
+    # after its memory was unmapped (host queries only).
+    import hiprt
+    ranges, outlived = cyclone_amd.debug_pin_history()
+    assert outlived == 0 and hiprt.OUTLIVED[0] == 0, \
+        "a host registration outlived its memory (library %d, tests %d)" % (outlived, hiprt.OUTLIVED[0])
+    assert not hiprt.LIVE, "test host registrations still live: %s" % hiprt.LIVE
+    stale = [(hex(lo), hi - lo) for lo, hi in ranges + hiprt.HISTORY if hiprt.answers_for(lo, hi)]
+    assert not stale, "the runtime still answers for released host ranges: %s" % stale
     fn = getattr(lib, "cyaes_debug_bounds", None)
     if fn is not None:
         rec = (ctypes.c_ulonglong * 20)()

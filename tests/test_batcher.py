@@ -750,16 +750,13 @@ def test_pool_in_foreign_registration(batcher):
     GPU unmapped pages, and one that starts on unpinned pages and
     runs into it is refused as well."""
     import numpy as np
-    import torch
-    cudart = torch.cuda.cudart()
-    if not hasattr(cudart, "cudaHostRegister"):
-        pytest.skip("torch.cuda.cudart() has no cudaHostRegister")
+    import hiprt
     key = _keys(1, 43)[0]
     slot = batcher.session_open(key)
     buf = np.zeros(8 * 4096, dtype=np.uint8)
     p0 = (-buf.ctypes.data) % 4096
     lo = buf.ctypes.data + p0 + 4096  # pages 1..4 of buf's page-aligned part, registered by "someone else"
-    assert int(cudart.cudaHostRegister(lo, 4 * 4096, 0)) == 0
+    assert hiprt.host_register(lo, 4 * 4096) == 0
     key_aes = oracle.Rijndael(key)
 
     def encrypt_in(pid, base, n, seed):
@@ -785,7 +782,7 @@ def test_pool_in_foreign_registration(batcher):
         encrypt_in(pid, p0 + 4096 + 64, 4096, 43)
         batcher.unregister_pool(pid)  # leaves the foreign registration alone
     finally:
-        assert int(cudart.cudaHostUnregister(lo)) == 0
+        assert hiprt.host_unregister(lo) == 0
     batcher.session_close(slot)
 
 

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import cyclone_amd as ca
+import hiprt
 import oracle
 
 pytestmark = pytest.mark.gpu
@@ -505,15 +506,12 @@ def test_host_batch_in_foreign_registrations(torch):
     assert np.array_equal(h_pin.numpy(), want)
     after, d = _pin_delta(before)
     assert d["registered"] == 0 and d["conflicts"] == 0 and after["live"] == 0
-    cudart = torch.cuda.cudart()
-    if not hasattr(cudart, "cudaHostRegister"):
-        pytest.skip("torch.cuda.cudart() has no cudaHostRegister")
     arena = np.zeros(total + 4 * 4096, dtype=np.uint8)
     off = (-arena.ctypes.data) % 4096 + 64
     buf = arena[off:off + total]
     buf[:] = pt
     lo = arena.ctypes.data + off - 64 + 2 * 4096  # pages 2..4 of the buffer, registered by "the caller"
-    assert int(cudart.cudaHostRegister(lo, 3 * 4096, 0)) == 0
+    assert hiprt.host_register(lo, 3 * 4096) == 0
     try:
         before = ca.debug_pins()
         c.encrypt_host(buf.ctypes.data, buf.ctypes.data, n, pb, chunk_bytes=256 * 1472)
@@ -523,7 +521,7 @@ def test_host_batch_in_foreign_registrations(torch):
         c.decrypt_host(buf.ctypes.data, buf.ctypes.data, n, pb)
         assert np.array_equal(buf, pt)
     finally:
-        assert int(cudart.cudaHostUnregister(lo)) == 0
+        assert hiprt.host_unregister(lo) == 0
     c.close()
 
 
@@ -567,6 +565,85 @@ def test_set_keys_waits_only_for_its_own_streams(torch):
     assert a.check() == ca.CYAES_OK
     a.close()
     b.close()
+
+
+def test_set_keys_device_back_to_back_on_two_streams(torch):
+    """Two cyaes_gpu_set_keys_device calls on two streams, the first queued
+    behind an ~8 ms decrypt of another context: the second key set wins,
+    bit-exactly (its expansion waits on the device for the first's; VERDICT r05
+    weak 5).  Per-session keys arrive by broadcast and are expanded where they
+    land (relay_server.cpp:218-240, a new Rijndael per session at :224,229)."""
+    n, pb = 65536, 65536
+    a, b = ca.GpuContext(0), ca.GpuContext(0)
+    a.set_keys(K0)
+    b.set_keys(K0)
+    ct = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
+    pt = torch.empty_like(ct)
+    b.fill_synthetic(ct, 0, n, pb, oracle.PLAINTEXT_SEED)
+    keys1 = [oracle.session_key(100 + i) for i in range(6)]
+    keys2 = [oracle.session_key(200 + i) for i in range(6)]
+    d1 = torch.from_numpy(np.frombuffer(b"".join(keys1), np.uint8).copy()).to("cuda")
+    d2 = torch.from_numpy(np.frombuffer(b"".join(keys2), np.uint8).copy()).to("cuda")
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    end = torch.cuda.Event()
+    with torch.cuda.stream(s1):
+        for _ in range(3):
+            b.decrypt_uniform(ct, pt, n, pb, stream=s1.cuda_stream)  # b's table: a's writes need not wait for it
+        a.set_keys_device(d1, 6, stream=s1.cuda_stream)
+        end.record(s1)
+    a.set_keys_device(d2, 6, stream=s2.cuda_stream)
+    queued_behind = not end.query()
+    for i in range(6):
+        assert a.get_key(i).words() == ca.key_expand(keys2[i]).words(), i
+    small = oracle.synthetic(7, 6 * 16, 1024)
+    d_in = torch.from_numpy(small.copy()).to("cuda")
+    d_out = torch.empty_like(d_in)
+    a.encrypt_uniform(d_in, d_out, 6 * 16, 1024, payloads_per_key=16)
+    assert np.array_equal(host(d_out), oracle.batch(False, keys2, 16, small, 1024))
+    assert queued_behind, "the first expansion was not still queued when the second was issued"
+    assert a.check() == ca.CYAES_OK
+    a.close()
+    b.close()
+
+
+def test_key_uses_bounded_over_short_lived_streams(torch):
+    """1,000 batches, each on a stream of its own created and destroyed around
+    it (a caller that opens a stream per request): the context's record of
+    streams reading its key table keeps only those with a batch in flight
+    (cyaes_debug_ctx), and a key write afterwards waits for nothing stale.
+    Every batch bit-exact."""
+    c = ca.GpuContext(0)
+    c.set_keys(K0)
+    n, pb = 64, 1024
+    pt = oracle.synthetic(8, n, pb)
+    want = oracle.batch(False, [K0], 0, pt, pb)
+    d_in = torch.from_numpy(pt.copy()).to("cuda")
+    outs = [torch.empty_like(d_in) for _ in range(4)]
+    torch.cuda.synchronize()
+    peak = 0
+    for i in range(1000):
+        s = hiprt.stream_create()
+        out = outs[i % 4]
+        if i % 2:
+            c.encrypt_uniform(d_in, out, n, pb, stream=s)
+        else:
+            c.encrypt_strided(d_in, out, 0, pb, n, pb, stream=s)
+        if i % 97 == 0:
+            hiprt.stream_sync(s)
+            assert np.array_equal(host(out), want), i
+        hiprt.stream_destroy(s)
+        peak = max(peak, c.debug_state()["key_uses"])
+    torch.cuda.synchronize()
+    c.encrypt_uniform(d_in, outs[0], n, pb)
+    torch.cuda.synchronize()
+    st = c.debug_state()
+    assert st["key_uses"] <= 1, st
+    assert peak < 200, peak  # (bounded by the batches in flight, not by the 1,000 streams)
+    c.update_keys(0, K0)  # waits for the one reader left
+    assert c.debug_state()["key_uses"] == 0
+    assert np.array_equal(host(outs[0]), want)
+    c.close()
 
 
 def test_host_batch_single_key_large(torch, ctx):
