@@ -23,9 +23,11 @@ its own passes.  No data-path collective.
 
 `--config A|B|C|D` run one BASELINE.json config per GPU instead (weak
 scaling: per-GPU batch fixed, payload range [rank*P, (rank+1)*P)).
-packet_configs: configs B (1 M x 1,472 B) and D (4,096 session keys x 256 x
-1,472 B), measured after the headline at the same GPU count with the same
-timing rules; reported beside `value`, never as it.
+packet_configs: configs A (the reference's own unit-test shape, 4,096 x
+1,024 B, cyt_unit_crypt.cpp:173-248), B (1 M x 1,472 B) and D (4,096 session
+keys x 256 x 1,472 B), measured after the headline at the same GPU count with
+the same timing rules, each with its CPU baseline (all usable cores and one
+core) at N = 1; reported beside `value`, never as it.
 
 roofline: the kernels are bound by LDS gather issue, so
 `bound` is "lds"; `frac` keeps the contract's definition (algorithmic bytes /
@@ -87,7 +89,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-clock", action="store_true", help="skip the in-kernel clock measurement")
-    ap.add_argument("--packet-configs", default="B,D",
+    ap.add_argument("--packet-configs", default="A,B,D",
                     help="other BASELINE.json packet configs measured after the headline one ('none' to skip)")
     ap.add_argument("--packet-steps", type=int, default=20)
     ap.add_argument("--relay-stream", type=int, default=1,
@@ -784,8 +786,9 @@ def main():
     main_res["d_ct"] = main_res["d_pt"] = None
     torch.cuda.empty_cache()
 
-    # The north star's other named packet sizes, at the same GPU count: MTU-sized
-    # payloads (config B) and per-session keys (config D).  Reported beside the
+    # The other BASELINE.json configs, at the same GPU count: the reference's
+    # unit-test shape (config A), MTU-sized payloads (config B) and per-session
+    # keys (config D).  Reported beside the
     # headline config, never as `value`.
     packet_configs = {}
     for name in ([] if args.packet_configs == "none" else args.packet_configs.split(",")):

@@ -985,11 +985,12 @@ int cyaes_batcher_register_pool(cyaes_batcher* b, void* base, size_t bytes, uint
     int dev_prev = 0;
     (void)hipGetDevice(&dev_prev);
     (void)hipSetDevice(b->cfg.device);
-    // Pin the whole pages the range covers (the caller's buffer need not be page aligned).
-    const uintptr_t lo = (uintptr_t)base & ~(uintptr_t)4095;
-    const uintptr_t hi = ((uintptr_t)base + bytes + 4095) & ~(uintptr_t)4095;
+    // The pool's exact bytes (the caller's buffer need not be page aligned):
+    // the registry registers the whole pages they cover, shared with other
+    // pools' registrations on the same pages, and tests a foreign registration
+    // on the bytes themselves.
     cyaes::PinHold held;
-    int st = cyaes::pin_acquire(lo, hi, cyaes::PinMode::kShared, &held);
+    int st = cyaes::pin_acquire((uintptr_t)base, (uintptr_t)base + bytes, cyaes::PinMode::kShared, &held);
     if (st == cyaes::kPinConflict) st = CYAES_EINVAL;  // part of the pages registered by another owner
     // The device view must be one contiguous range: check it at the end and at
     // every boundary between the registrations that hold the pool.

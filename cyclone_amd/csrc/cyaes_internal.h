@@ -249,7 +249,7 @@ int ragged_batch(cyaes_gpu* ctx, bool decrypt, const uint32_t* d_table, uint32_t
 constexpr uintptr_t kPinPage = 4096;
 constexpr int kPinConflict = 1;  // internal: pages another owner (or a host batch) holds
 enum class PinMode {
-    kShared,     // a batcher pool: page-aligned span, shared with other pools' registrations by reference count
+    kShared,     // a batcher pool: its pages registered, shared with other pools' registrations by reference count
     kExclusive,  // a host batch's buffer: the exact byte range, on pages no other registration touches
 };
 struct PinHold {

@@ -151,7 +151,6 @@ int pin_acquire(uintptr_t lo, uintptr_t hi, PinMode mode, PinHold* h) {
     h->foreign = false;
     if (lo >= hi) return CYAES_EINVAL;
     const bool shared = mode == PinMode::kShared;
-    if (shared && ((lo | hi) & (kPinPage - 1))) return CYAES_EINVAL;
     const uintptr_t plo = page_down(lo), phi = page_up(hi);
     Registry& r = reg();
     std::lock_guard<std::mutex> lk(r.mu);
@@ -169,7 +168,10 @@ int pin_acquire(uintptr_t lo, uintptr_t hi, PinMode mode, PinHold* h) {
         c = std::max(c, it->second.phi);
     }
     if (c < phi) gaps.push_back({c, phi});
-    if (ours.empty() && inside_one_foreign(lo, hi)) {  // memory someone else registered: used as it is
+    // Memory someone else registered, used as it is: the test runs on the exact
+    // bytes (a pool at the tail of a registration whose size is not
+    // a page multiple lies inside it, its page span does not).
+    if (ours.empty() && inside_one_foreign(lo, hi)) {
         h->foreign = true;
         return CYAES_OK;
     }

@@ -39,6 +39,8 @@ def runtime():
         rt.hipStreamDestroy.argtypes = [vp]
         rt.hipStreamSynchronize.argtypes = [vp]
         rt.hipGetLastError.argtypes = []
+        rt.hipHostMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_uint]
+        rt.hipHostFree.argtypes = [vp]
         _rt = rt
     return _rt
 
@@ -90,6 +92,18 @@ def answers_for(lo, hi):
         return False
     plo, phi = lo & ~(PAGE - 1), (hi + PAGE - 1) & ~(PAGE - 1)
     return ((base.value or 0), size.value) in ((lo, hi - lo), (plo, phi - plo))
+
+
+def host_malloc(nbytes):
+    """hipHostMalloc (pinned, mapped): an allocation of exactly nbytes as the runtime records it."""
+    p = ctypes.c_void_p()
+    st = int(runtime().hipHostMalloc(ctypes.byref(p), nbytes, 0))
+    assert st == 0, "hipHostMalloc: %d" % st
+    return p.value
+
+
+def host_free(p):
+    assert int(runtime().hipHostFree(p)) == 0
 
 
 def stream_create(nonblocking=True):

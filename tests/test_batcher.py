@@ -786,6 +786,39 @@ def test_pool_in_foreign_registration(batcher):
     batcher.session_close(slot)
 
 
+def test_pool_at_the_tail_of_a_foreign_allocation(batcher):
+    """A pool whose last byte is the last byte of another owner's pinned
+    allocation, whose size is not a page multiple (hipHostMalloc of 3 pages +
+    100 B): it lies inside that registration and is used as it is, nothing
+    registered (the registry tests the pool's exact bytes, not its
+    page span, which reaches past the allocation).  Bit-exact."""
+    import ctypes
+    import numpy as np
+    import hiprt
+    key = _keys(1, 47)[0]
+    slot = batcher.session_open(key)
+    aes = oracle.Rijndael(key)
+    size = 3 * 4096 + 100
+    p = hiprt.host_malloc(size)
+    try:
+        buf = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(p))
+        tail = buf[size - 1000:]
+        before = ca.debug_pins()
+        pid = batcher.register_pool(tail)
+        after = ca.debug_pins()
+        assert after["registered"] == before["registered"] and after["conflicts"] == before["conflicts"]
+        data = bytes(random.Random(47).getrandbits(8) for _ in range(992))
+        tail[8:1000] = np.frombuffer(data, np.uint8)
+        assert batcher.submit_pooled([(ca.OP_ENCRYPT, slot, pid, 8, 8, 992, None, 0)]) == [0]
+        assert batcher.flush() == ca.CYAES_OK
+        assert bytes(tail[8:1000]) == bytes(aes.encrypt(bytearray(data)))
+        batcher.unregister_pool(pid)
+        assert ca.debug_pins()["live"] == 0
+    finally:
+        hiprt.host_free(p)
+    batcher.session_close(slot)
+
+
 def test_pooled_open_range_and_unregister_flush(batcher):
     """A pooled OPEN whose packet would run past its pool is refused before
     its header is read, and unregister_pool, which drains the
