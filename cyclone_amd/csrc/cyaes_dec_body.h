@@ -213,7 +213,7 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
 #pragma unroll
     for (int k = 0; k < R; k++) d[k] = pv[k];
     if (!KEYED) {
-        dec_cbc<R>(lds, lo, dk0, c, d);  // all R rows per LDS round trip (A/B: ~1% over 2 rows)
+        dec_cbc<R>(lds, lo, dk0, c, d, si_bytes(a.tables));  // all R rows per LDS round trip (A/B: ~1% over 2 rows)
     } else {
         uint32_t kid[R];
         bool valid[R];
@@ -241,7 +241,7 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
                 load_sched(a.keys, k0, 1, dk0);
                 dk_id = k0;
             }
-            dec_cbc<R>(lds, lo, dk0, c, d);
+            dec_cbc<R>(lds, lo, dk0, c, d, si_bytes(a.tables));
         } else {
 #pragma unroll
             for (int k = 0; k < R; k++) {
@@ -256,7 +256,7 @@ __device__ __forceinline__ uint4 flat_step(const DecArgs& a, const char* lds, ui
                         load_sched(a.keys, ku, 1, dk);
                         const uint4 cc[1] = {c[k]};
                         uint4 dd[1] = {d[k]};
-                        dec_cbc<1>(lds, lo, dk, cc, dd);
+                        dec_cbc<1>(lds, lo, dk, cc, dd, si_bytes(a.tables));
                         d[k] = dd[0];
                     }
                 }

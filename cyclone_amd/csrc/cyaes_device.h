@@ -274,9 +274,33 @@ __device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg(
 
 // Decrypts N independent blocks together (N-way ILP per LDS round trip) and
 // returns D(c[n]) ^ prev[n] in prev[n] (CBC, cyr_rijndael.cpp:625-630).
+// A/B variant (r06), measured and not kept: the last
+// round's 16 Si lookups per block from global memory (the TA path) instead of
+// the LDS, so they would run beside the LDS gathers.  They do not: independent
+// VMEM gathers from a small table sustain ~2.5 lookups / clk / CU against the
+// LDS's ~27 (tools/microbench.hip k_vmix: 4 VMEM gathers per 16 LDS lookups
+// cut the LDS rate from 26.6 to 10.1 per clk), and the decrypt needs ~3 Si
+// lookups / clk / CU: config C decrypt 11.12 -> 13.38 ms, config B 1.024 ->
+// 1.264 ms, bit-exact (profiles/r06/vmem/).
+#ifndef CYAES_DEC_SI_VMEM
+#define CYAES_DEC_SI_VMEM 0
+#endif
+// The inverse S-box bytes in global memory (kSiOff), from a decrypt's table pointer (kDecTableOff).
+__device__ __forceinline__ const uint8_t* si_bytes(const uint32_t* dec_tables) {
+    return reinterpret_cast<const uint8_t*>(dec_tables) + (kSiOff - kDecTableOff);
+}
+// Last-round word from global memory: Si[byte k of x_k] in byte k (the LDS
+// form is dec_last).  global_load_ubyte gathers from one 256-B table: two
+// 128-B lines, L1 resident; served by the TA path beside the LDS.
+__device__ __forceinline__ uint32_t dec_last_g(const uint8_t* __restrict__ si, uint32_t x0, uint32_t x1, uint32_t x2,
+                                               uint32_t x3) {
+    const uint32_t l0 = si[x0 & 0xFFu], l1 = si[(x1 >> 8) & 0xFFu], l2 = si[(x2 >> 16) & 0xFFu], l3 = si[x3 >> 24];
+    return l0 | (l1 << 8) | (l2 << 16) | (l3 << 24);
+}
+
 template <int N>
 __device__ __forceinline__ void dec_cbc(const char* lds, uint32_t lo, const uint32_t* __restrict__ dk,
-                                        const uint4 (&c)[N], uint4 (&prev)[N]) {
+                                        const uint4 (&c)[N], uint4 (&prev)[N], const uint8_t* __restrict__ gsi = nullptr) {
     uint32_t s[N][4];
 #pragma unroll
     for (int n = 0; n < N; n++) {
@@ -298,6 +322,17 @@ __device__ __forceinline__ void dec_cbc(const char* lds, uint32_t lo, const uint
 #pragma unroll
             for (int j = 0; j < 4; j++) s[n][j] = t[n][j];
     }
+#if CYAES_DEC_SI_VMEM
+    if (gsi) {
+#pragma unroll
+        for (int n = 0; n < N; n++)
+            prev[n] = make_uint4(xor3(dec_last_g(gsi, s[n][0], s[n][3], s[n][2], s[n][1]), dk[40], prev[n].x),
+                                 xor3(dec_last_g(gsi, s[n][1], s[n][0], s[n][3], s[n][2]), dk[41], prev[n].y),
+                                 xor3(dec_last_g(gsi, s[n][2], s[n][1], s[n][0], s[n][3]), dk[42], prev[n].z),
+                                 xor3(dec_last_g(gsi, s[n][3], s[n][2], s[n][1], s[n][0]), dk[43], prev[n].w));
+        return;
+    }
+#endif
 #pragma unroll
     for (int n = 0; n < N; n++) {
         const uint32_t lsi = (lo & 0xFFu) | 0x20000u;  // lane bits | 128 KiB (Si image)

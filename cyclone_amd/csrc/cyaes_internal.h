@@ -34,7 +34,8 @@ constexpr int kDecTableWords = 768;  // TL5[256], TL7[256], SiW[256]
 constexpr int kEncTableOff = 0;
 constexpr int kDecTableOff = kEncTableWords * 4;
 constexpr int kSboxOff = kDecTableOff + kDecTableWords * 4;
-constexpr int kTablesBytes = kSboxOff + 256;
+constexpr int kSiOff = kSboxOff + 256;  // inverse S-box bytes (global-memory Si lookups, CYAES_DEC_SI_VMEM)
+constexpr int kTablesBytes = kSiOff + 256;
 
 // Workgroup shapes: 16 waves x 1 WG/CU (128 / 160 KiB LDS) for both directions.
 constexpr int kEncThreads = 1024;

@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                 }
             }
             if (!KEYED) {
-                dec_cbc<R>(lds, lo, dk0, c, pv);
+                dec_cbc<R>(lds, lo, dk0, c, pv, si_bytes(a.tables));
             } else {
                 uint32_t kid[R];
 #pragma unroll
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                         load_sched(a.keys, k0, 1, dk0);
                         dk_id = k0;
                     }
-                    dec_cbc<R>(lds, lo, dk0, c, pv);
+                    dec_cbc<R>(lds, lo, dk0, c, pv, si_bytes(a.tables));
                 } else {
 #pragma unroll
                     for (int k = 0; k < R; k++) {
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
                                 load_sched(a.keys, ku, 1, dk);
                                 const uint4 cc[1] = {c[k]};
                                 uint4 dd[1] = {pv[k]};
-                                dec_cbc<1>(lds, lo, dk, cc, dd);
+                                dec_cbc<1>(lds, lo, dk, cc, dd, si_bytes(a.tables));
                                 pv[k] = dd[0];
                             }
                         }

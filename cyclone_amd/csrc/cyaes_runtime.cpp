@@ -713,6 +713,7 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     memcpy(host + kEncTableOff, t.enc, sizeof(t.enc));
     memcpy(host + kDecTableOff, t.dec, sizeof(t.dec));
     memcpy(host + kSboxOff, t.sbox, 256);
+    memcpy(host + kSiOff, t.inv_sbox, 256);
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tables), kTablesBytes);
     if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, host, kTablesBytes, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_status), 16);

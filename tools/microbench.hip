@@ -113,6 +113,63 @@ __global__ __launch_bounds__(1024, 1) void k_mix(uint32_t* out, int iters, Clk* 
     }
 }
 
+// Independent VMEM gathers beside the LDS stream: per
+// iteration the 16 LDS chains of k_lds<0>, plus NV gathers from a 1 KiB
+// global table whose addresses come from the LDS chains' state and whose
+// results feed only an accumulator -- never an address, as the decrypt's
+// last-round Si lookups feed only the store (cyr_rijndael.cpp:753-773).  DIST
+// 0: consumed at the end of the iteration that issued them; 1: one iteration
+// later.  If the TA path runs in parallel with the LDS, the LDS lookup rate
+// stays at k_lds<0>'s while NV extra lookups per 16 ride along.
+template <int NV, int DIST>
+__global__ __launch_bounds__(1024, 1) void k_vmix(uint32_t* out, int iters, Clk* clk, const uint32_t* __restrict__ gtab) {
+    __shared__ uint32_t lds[24576];  // 96 KiB: one workgroup per CU
+    for (int i = threadIdx.x; i < 24576; i += blockDim.x) lds[i] = i * 2654435761u;
+    __syncthreads();
+    const uint32_t lo = (threadIdx.x & 31u) << 2;
+    uint32_t s[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) s[j] = (threadIdx.x * 7919u + j * 104729u) | 1;
+    uint32_t acc = 0, held[NV > 0 ? NV : 1] = {};
+    unsigned long long t0 = 0, r0 = 0;
+    if (threadIdx.x == 0) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    for (int it = 0; it < iters; it++) {
+        uint32_t vv[NV > 0 ? NV : 1];
+#pragma unroll
+        for (int k = 0; k < NV; k++) vv[k] = gtab[(s[k] >> (8 * (k & 3))) & 0xFF];
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t a = __builtin_amdgcn_perm(s[j], lo, 0x0C0C0400u + ((j & 3) << 8));
+            v[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + a);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) s[j] ^= v[j];
+#pragma unroll
+        for (int k = 0; k < NV; k++) {
+            if (DIST == 0) acc ^= vv[k];
+            else {
+                acc ^= held[k];
+                held[k] = vv[k];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NV; k++) acc ^= held[k];
+#pragma unroll
+    for (int j = 0; j < 16; j++) acc ^= s[j];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+    if (threadIdx.x == 0) {
+        clk[blockIdx.x].t0 = t0;
+        clk[blockIdx.x].r0 = r0;
+        clk[blockIdx.x].t1 = __builtin_amdgcn_s_memtime();
+        clk[blockIdx.x].r1 = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // LDS peak: one v_perm per 4 conflict-free ds_read_b32 (offsets 0/64/128/192)
 // and one xor3 per 2 reads, so VALU cannot bind.  B64: ds_read_b64 instead.
 template <bool B64>
@@ -316,6 +373,17 @@ int main() {
     CHECK(hipMalloc(&d_tab, 1024));
     CHECK(hipMemset(d_tab, 0x5a, 1024));
     g_tab = d_tab;
+    if (getenv("MB_ONLY_VMIX")) {
+        // rates in LDS lookups per clk per CU (the VMEM gathers ride along)
+        run("vmix_lds16", k_vmix<0, 0>, 1024, it, 16, "lds lookups", cus, d_out, d_clk);
+        run("vmix_lds16_vmem2_d0", k_vmix<2, 0>, 1024, it, 16, "lds lookups", cus, d_out, d_clk);
+        run("vmix_lds16_vmem2_d1", k_vmix<2, 1>, 1024, it, 16, "lds lookups", cus, d_out, d_clk);
+        run("vmix_lds16_vmem4_d0", k_vmix<4, 0>, 1024, it, 16, "lds lookups", cus, d_out, d_clk);
+        run("vmix_lds16_vmem4_d1", k_vmix<4, 1>, 1024, it, 16, "lds lookups", cus, d_out, d_clk);
+        run("vmix_lds16_vmem8_d1", k_vmix<8, 1>, 1024, it, 16, "lds lookups", cus, d_out, d_clk);
+        run("vmix_lds16_vmem16_d1", k_vmix<16, 1>, 1024, it, 16, "lds lookups", cus, d_out, d_clk);
+        return 0;
+    }
     if (getenv("MB_ONLY_BPERM")) {
         run("bperm0_lds16", k_bperm<0>, 1024, it, 16, "lookups", cus, d_out, d_clk);
         run("bperm4_lds12", k_bperm<4>, 1024, it, 16, "lookups", cus, d_out, d_clk);
