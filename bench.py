@@ -67,6 +67,31 @@ CONFIGS = {
     "A": (4096, 1024, 0),
 }
 E_PASS_PAYLOADS, E_PASSES, E_PAYLOAD_BYTES = 262144, 32, 65536  # 32 x 2^18 = 2^23 payloads
+MIXED_SEED = 0xFF00  # relay_stream.mixed layout (tests/golden/relay_mixed.json)
+RELAY_MAX_CHUNK = 0xFF00
+
+
+def mixed_stream_layout(total_bytes, seed=MIXED_SEED):
+    """A relay tunnel stream of mixed packet sizes (relay_local.cpp:188-206):
+    the client's socket delivers reads of r bytes (uniform in 1 .. 4 x 0xFF00,
+    drawn with `seed`) until total_bytes are sent; each read goes out as chunks
+    of min(rest, 0xFF00) bytes, each in a packet of a 4-B header, an 8-B
+    RelayForwardMsg and the chunk rounded up to 16 B (encrypted in place),
+    packets back to back.  Returns (payload offsets uint64, payload bytes
+    uint32, stream bytes rounded up to 16)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    sizes, rest = [], total_bytes
+    while rest > 0:
+        r = min(rest, int(rng.integers(1, 4 * RELAY_MAX_CHUNK + 1)))
+        rest -= r
+        full, tail = divmod(r, RELAY_MAX_CHUNK)
+        sizes += [RELAY_MAX_CHUNK] * full + ([tail] if tail else [])
+    chunk = np.array(sizes, dtype=np.uint64)
+    nbytes = ((chunk + 15) // 16 * 16).astype(np.uint32)
+    pkt = nbytes.astype(np.uint64) + 12
+    offsets = (np.cumsum(pkt) - pkt + 12).astype(np.uint64)
+    return offsets, nbytes, int((int(pkt.sum()) + 15) // 16 * 16)
 
 
 def log(*a):
@@ -531,6 +556,76 @@ def main():
             del d_ct, d_pt
         return res
 
+    def run_mixed_stream():
+        """relay_stream.mixed: config B's bytes as a relay tunnel stream of
+        mixed packet sizes (mixed_stream_layout: full 0xFF00 chunks and the
+        reads' tails, relay_local.cpp:188-206), encrypted then decrypted in
+        place through the ragged entry points (device offset / size lists), as
+        the relay's sender (relay_local.cpp:206) and receiver
+        (relay_server.cpp:329) would hand a parsed stream over.  Every GPU the
+        same stream (weak scaling).  Parity: digests of the whole stream buffer
+        against tests/golden/relay_mixed.json (oracle-derived)."""
+        import numpy as np
+        offsets, nbytes, alloc = mixed_stream_layout(CONFIGS["B"][0] * CONFIGS["B"][1])
+        n = int(offsets.size)
+        payload = int(nbytes.sum())
+        set_session_keys(0, 1, 0)
+        mbuf = torch.empty(alloc, dtype=torch.uint8, device="cuda")
+        d_off = torch.from_numpy(offsets.astype(np.int64)).to("cuda")
+        d_nb = torch.from_numpy(nbytes.astype(np.int32)).to("cuda")
+        ctx.fill_synthetic(mbuf, 0, alloc // 16, 16, PLAINTEXT_SEED, sh)
+
+        def dig():
+            return ["%016x" % v for v in ctx.digest(mbuf, alloc, sh)]
+
+        def m_enc():
+            ctx.encrypt_ragged(mbuf, mbuf, d_off, d_nb, n, stream=sh)
+
+        def m_dec():
+            ctx.decrypt_ragged(mbuf, mbuf, d_off, d_nb, n, stream=sh)
+        mpar = None
+        if not args.no_verify:
+            gm = json.load(open(os.path.join(ROOT, "tests", "golden", "relay_mixed.json")))
+            ok = gm["packets"] == n and gm["stream_bytes"] == alloc and dig() == gm["plain_digest"]
+            m_enc()
+            ok = ok and ctx.check() == ca.CYAES_OK and dig() == gm["cipher_digest"]
+            m_dec()
+            ok = ok and ctx.check() == ca.CYAES_OK and dig() == gm["plain_digest"]
+            mpar = "bit-exact" if all_ok(ok) else "MISMATCH"
+        for _ in range(args.packet_warmup):
+            m_enc()
+            m_dec()
+        mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+                torch.cuda.Event(enable_timing=True)) for _ in range(args.packet_steps)]
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.packet_steps):
+            mev[i][0].record(stream)
+            m_enc()
+            mev[i][1].record(stream)
+            m_dec()
+            mev[i][2].record(stream)
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        mt = max_over_ranks(time.perf_counter() - t0)
+        out = {
+            "value": round(2.0 * payload * args.packet_steps * world / mt / gib, 2), "unit": "GiB/s",
+            "encrypt_ms": round(sum(a.elapsed_time(b) for a, b, _ in mev) / args.packet_steps, 4),
+            "decrypt_ms": round(sum(b.elapsed_time(c) for _, b, c in mev) / args.packet_steps, 4),
+            "parity": mpar, "packets": n, "payload_bytes": payload,
+            "full_chunks": int((nbytes == RELAY_MAX_CHUNK).sum()),
+            "layout": "config B's %d bytes as relay chunks: socket reads uniform in 1..4 x 0xFF00 B, each sent as "
+                      "0xFF00-B chunks plus its tail, payload = chunk rounded to 16 at packet offset 12, packets back "
+                      "to back, in place, cyaes_gpu_{en,de}crypt_ragged" % (CONFIGS["B"][0] * CONFIGS["B"][1]),
+            "parity_note": "digest of the whole stream buffer vs tests/golden/relay_mixed.json (oracle)",
+        }
+        del mbuf, d_off, d_nb
+        torch.cuda.empty_cache()
+        return out
+
     def run_e(steps, warmup, verify):
         """Config E: the whole job's fixed passes, this rank's share (see module doc)."""
         pp, passes, pb = args.e_pass_payloads, args.e_passes, E_PAYLOAD_BYTES
@@ -882,7 +977,56 @@ def main():
                 "decrypt_ms": round(sum(b.elapsed_time(c) for _, b, c in rev) / args.packet_steps, 4),
                 "parity": rpar,
             }
-        relay = dict(relay["strided"], ragged=relay["ragged"], api="cyaes_gpu_{en,de}crypt_strided "
+        # Both directions of a relay end at once (relay_server.cpp:472 encrypts
+        # target -> tunnel while :329 decrypts tunnel -> target): the sent stream
+        # encrypted while the received one is decrypted, one launch per step
+        # (cyaes_gpu_duplex_strided) against the two strided calls above.
+        buf2 = torch.full_like(buf, 0xA5)
+        view2 = buf2[: rn * stride].view(rn, stride)
+        view2[:, hdr:hdr + rpb] = d_pt.view(rn, rpb)
+        ctx.encrypt_strided(buf2, buf2, hdr, stride, rn, rpb, stream=sh)  # the received stream: ciphertext
+
+        def r_dup():
+            ctx.duplex_strided(buf, buf, hdr, stride, rn, rpb, buf2, buf2, hdr, stride, rn, rpb, stream=sh)
+        dpar = None
+        if not args.no_verify:
+            view[:, hdr:hdr + rpb] = d_pt.view(rn, rpb)
+            ct2 = view2[:, hdr:hdr + rpb].contiguous()
+            r_dup()
+            ok = ctx.check() == ca.CYAES_OK and bool(torch.equal(view[:, hdr:hdr + rpb], ct2))
+            ok = ok and bool(torch.equal(view2[:, hdr:hdr + rpb].reshape(-1), d_pt))
+            ok = ok and bool((view[:, :hdr] == 0xA5).all()) and bool((view2[:, :hdr] == 0xA5).all())
+            g = golden.get("B") if rank == 0 else None
+            if g and g["npayloads"] == rn and g["p0"] == p0:
+                ok = ok and ["%016x" % v for v in ctx.digest(ct2, rn * rpb, sh)] == g["cipher_digest"]
+            del ct2
+            dpar = "bit-exact" if all_ok(ok) else "MISMATCH"
+        for _ in range(args.packet_warmup):
+            r_dup()
+        dev_ = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(args.packet_steps)]
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.packet_steps):
+            dev_[i][0].record(stream)
+            r_dup()
+            dev_[i][1].record(stream)
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        dt = max_over_ranks(time.perf_counter() - t0)
+        relay["duplex"] = {
+            "value": round(2.0 * rn * rpb * args.packet_steps * world / dt / gib, 2), "unit": "GiB/s",
+            "ms_per_step": round(sum(a.elapsed_time(b) for a, b in dev_) / args.packet_steps, 4),
+            "parity": dpar,
+            "api": "cyaes_gpu_duplex_strided: one stream of the layout encrypted while a second one is decrypted, "
+                   "one launch (+ its prepass) per step; compare encrypt_ms + decrypt_ms of the strided calls",
+        }
+        del buf2, view2
+        relay = dict(relay["strided"], ragged=relay["ragged"], duplex=relay["duplex"],
+                     api="cyaes_gpu_{en,de}crypt_strided "
                      "(cyaes_relay_stride finds the stream equally strided); `ragged`: the same stream through "
                      "cyaes_gpu_{en,de}crypt_ragged with device offset / size lists",
                      layout="config B payloads (%d x %d B per GPU) at packet offset %d, packet stride %d B, in place"
@@ -892,6 +1036,7 @@ def main():
                                  "headers untouched; decrypt restores the plaintext")
         del buf, view, d_pt, d_off, d_nb
         torch.cuda.empty_cache()
+        relay["mixed"] = run_mixed_stream()
 
     if rank == 0:
         if args.config == "E":

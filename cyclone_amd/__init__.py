@@ -97,6 +97,10 @@ _SIGS = {
     "cyaes_debug_pin_history": (ctypes.c_uint64, [_u64p, ctypes.c_uint64, _u64p]),
     "cyaes_gpu_duplex_uniform": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                                 _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp]),
+    "cyaes_gpu_duplex_strided": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64,
+                                                ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                                _vp]),
     # include/cyaes_relay.h
     "cyaes_relay_round16": (ctypes.c_uint32, [ctypes.c_uint32]),
     "cyaes_relay_packet_bytes": (ctypes.c_uint32, [ctypes.c_uint32]),
@@ -378,6 +382,14 @@ class GpuContext:
         _check(self._lib.cyaes_gpu_duplex_uniform(self._h, _p(enc_in), _p(enc_out), enc_npayloads, enc_payload_bytes,
                                                   enc_key, _p(dec_in), _p(dec_out), dec_npayloads, dec_payload_bytes,
                                                   dec_key, _p(stream)), "duplex_uniform")
+
+    def duplex_strided(self, enc_in, enc_out, enc_first, enc_stride, enc_npayloads, enc_payload_bytes, dec_in, dec_out,
+                       dec_first, dec_stride, dec_npayloads, dec_payload_bytes, enc_key=0, dec_key=0, stream=None):
+        """Encrypt one relay stream and decrypt another in one launch (cyaes_gpu_duplex_strided)."""
+        _check(self._lib.cyaes_gpu_duplex_strided(self._h, _p(enc_in), _p(enc_out), enc_first, enc_stride,
+                                                  enc_npayloads, enc_payload_bytes, enc_key, _p(dec_in), _p(dec_out),
+                                                  dec_first, dec_stride, dec_npayloads, dec_payload_bytes, dec_key,
+                                                  _p(stream)), "duplex_strided")
 
     def encrypt_ragged(self, d_in, d_out, offsets, nbytes, npayloads, key_idx=None, payloads_per_key=0,
                        iv_in=None, iv_out=None, stream=None):

@@ -26,11 +26,16 @@
 
 #include "cyaes_dec_body.h"
 #include "cyaes_enc_body.h"
+#include "cyaes_lines_body.h"
 
 namespace cyaes {
 namespace {
 
-template <bool ERUNS, bool DBIG, uint32_t DIV>
+// LINES: the relay-stream form (cyaes_gpu_duplex_strided): the encrypt half
+// is a strided stream walked by 64-B lines (cyaes_lines_body.h, whole
+// 1,024-payload groups) and the decrypt half a strided stream walked by the
+// flat kernel's STRIDED rows.
+template <bool ERUNS, bool DBIG, uint32_t DIV, bool LINES = false>
 __global__ __launch_bounds__(kDecThreads, 1) void k_duplex(DuplexArgs x) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
     const char* lds = reinterpret_cast<const char*>(lds_words);
@@ -43,7 +48,8 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_duplex(DuplexArgs x) {
         __syncthreads();
         {
             CLOCK_PROBE(0);  // (probe builds: the encrypt phase as kind 0)
-            enc_body<false, false, ERUNS, false>(x.e, lds, elead);
+            if (LINES) lines_walk(x.e, lds, elead);
+            else enc_body<false, false, ERUNS, false>(x.e, lds, elead);
         }
         __syncthreads();  // all 16 waves are done with the encrypt image
     }
@@ -53,16 +59,23 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_duplex(DuplexArgs x) {
     if (threadIdx.x == 0) *leadp = 0;
     __syncthreads();
     CLOCK_PROBE(1);  // (the decrypt phase as kind 1)
-    dec_flat_body<false, DBIG, false, false, false, DIV, (uint32_t)offsetof(DuplexArgs, d)>(x.d, lds, leadp);
+    dec_flat_body<false, DBIG, false, false, LINES, DIV, (uint32_t)offsetof(DuplexArgs, d)>(x.d, lds, leadp);
 }
 
-template <bool ERUNS, bool DBIG>
+template <bool ERUNS, bool DBIG, bool LINES = false>
 void launch_div(const DuplexArgs& x, dim3 g, dim3 b, hipStream_t stream) {
-    if (x.d.prio_short) hipLaunchKernelGGL((k_duplex<ERUNS, DBIG, kDecPrioDivShort>), g, b, 0, stream, x);
-    else hipLaunchKernelGGL((k_duplex<ERUNS, DBIG, kDecPrioDiv>), g, b, 0, stream, x);
+    if (x.d.prio_short) hipLaunchKernelGGL((k_duplex<ERUNS, DBIG, kDecPrioDivShort, LINES>), g, b, 0, stream, x);
+    else hipLaunchKernelGGL((k_duplex<ERUNS, DBIG, kDecPrioDiv, LINES>), g, b, 0, stream, x);
 }
 
 }  // namespace
+
+hipError_t launch_duplex_lines(const DuplexArgs& x, int grid, hipStream_t stream) {
+    const dim3 g(grid), b(kDecThreads);
+    if (x.d.bpp.d >= 64u * kDecRows) launch_div<false, true, true>(x, g, b, stream);
+    else launch_div<false, false, true>(x, g, b, stream);
+    return hipGetLastError();
+}
 
 hipError_t launch_duplex(const DuplexArgs& x, int grid, hipStream_t stream) {
     const dim3 g(grid), b(kDecThreads);

@@ -178,6 +178,9 @@ hipError_t launch_decrypt_ragged(const DecArgs& a, int grid, int threads, hipStr
 // The flat decrypt's per-payload-key instantiations (cyaes_ragged_kernels.hip): for launch_decrypt_flat.
 void launch_decrypt_flat_keyed(const DecArgs& a, dim3 g, dim3 b, hipStream_t stream);
 hipError_t launch_duplex(const DuplexArgs& x, int grid, hipStream_t stream);  // 1024-thread workgroups
+// Relay streams: x.e strided, unkeyed, whole kLinesGroup groups (the lines
+// walk); x.d strided (the flat kernel's STRIDED rows), dyn on.
+hipError_t launch_duplex_lines(const DuplexArgs& x, int grid, hipStream_t stream);
 // Before a decrypt: zeroes its work words and, for an in-place flat decrypt
 // (boundary != NULL), snapshots C[begin-1] of every range that starts inside a payload.
 hipError_t launch_dec_prepass(const DecArgs& a, uint32_t work_words, hipStream_t stream);

@@ -39,6 +39,12 @@ __device__ __forceinline__ uint64_t rlane64(uint64_t v, uint32_t l) {
     return (uint64_t)hi << 32 | lo;
 }
 
+#ifndef CYAES_DEC_RAGGED_DIV
+// The progress-feedback divisor: the short-launch one (a relay stream's ragged
+// decrypt has ~92 steps per wave; r06 A/B at 8 / 4 / 2: 1.161 / 1.153 / 1.144
+// ms, profiles/r06/ab3/ragdiv.txt).
+#define CYAES_DEC_RAGGED_DIV kDecPrioDivShort
+#endif
 template <bool KEYED>
 __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
     constexpr int R = kDecRows;
@@ -90,9 +96,18 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
         const uint32_t nb0 = __builtin_amdgcn_readfirstlane(nbh);  // lane 0 holds a payload
         const uint64_t off0 = rlane64(offh, 0);
         const uint64_t ostr = gn > 1 ? rlane64(offh, 1) - off0 : 0;
-        const bool regular =
-            nb0 >= 64 && __ballot(holder && (nbh != nb0 || offh != off0 + (uint64_t)lane * ostr)) == 0;
+        // (r06) A regular group's rows are addressed as 32-bit offsets from its
+        // first payload (a scalar base), advanced by an add per row plus the
+        // packet gap at a payload boundary, as the flat kernel's strided rows
+        // are: no 64-bit multiply-add per row.  Groups spanning 4 GiB or more
+        // take the general path.
+        const bool regular = nb0 >= 64 && (uint64_t)gn * ostr < (1ull << 32) &&
+                             __ballot(holder && (nbh != nb0 || offh != off0 + (uint64_t)lane * ostr)) == 0;
         uint32_t jt = 0, rt = lane - 64u;  // regular: this lane's payload and block; the first row adds 64
+        uint32_t ro = 16u * (lane - 64u);  // regular: jt * ostr + 16 rt, mod 2^32
+        const uint32_t gap = (uint32_t)ostr - 16u * nb0;  // regular: bytes from a payload's end to the next one's start
+        const uint8_t* gin = a.in + off0;  // regular: the group's first payload (wave-uniform)
+        uint8_t* gout = a.out + off0;
         // Inclusive prefix of the group's block counts (64-bit: payloads may be up to 2^28 blocks).
         uint64_t incl = nbh;
         if (!regular) {
@@ -110,18 +125,22 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
             uint4 c[R], pv[R];
             uint32_t jr[R], rr[R];
             uint64_t orow[R];
+            uint32_t o32[R];
             bool valid[R];
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 if (regular) {
                     rt += 64;
-                    if (rt >= nb0) rt -= nb0, jt++;
+                    ro += 1024u;
+                    if (rt >= nb0) rt -= nb0, jt++, ro += gap;
                     valid[k] = jt < gn;
                     rr[k] = rt;
                     jr[k] = jt;
-                    orow[k] = off0 + (uint64_t)jt * ostr + 16ull * rt;
+                    o32[k] = ro;
+                    orow[k] = 0;
                     continue;
                 }
+                o32[k] = 0;
                 const uint64_t rlo = base + 64 * k;
                 const uint64_t g = rlo + lane;
                 valid[k] = g < total;
@@ -173,13 +192,19 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
             // group's end loads row 0 lane 0's block (always valid) and its result
             // is never used (a valid lane's predecessor is valid).  A load under
             // `valid ? load : 0` joined the branches with a vmcnt(0) wait per row.
-            const uint64_t safe = rlane64(orow[0], 0);
+            if (regular) {  // (as below: an invalid lane loads row 0 lane 0's block)
+                const uint32_t safe32 = __builtin_amdgcn_readlane(o32[0], 0);
 #pragma unroll
-            for (int k = 0; k < R; k++) c[k] = LD16U(a.in + (valid[k] ? orow[k] : safe), re[k]);
+                for (int k = 0; k < R; k++) c[k] = LD16U(gin + (valid[k] ? o32[k] : safe32), re[k]);
+            } else {
+                const uint64_t safe = rlane64(orow[0], 0);
+#pragma unroll
+                for (int k = 0; k < R; k++) c[k] = LD16U(a.in + (valid[k] ? orow[k] : safe), re[k]);
+            }
             // The progress atomic (a global word: the decrypt image fills the LDS) goes
             // out after the step's loads, so its round trip overlaps theirs instead of
             // delaying them (A/B: -1 % on relay streams, profiles/r02/ab_ragged_prio_late.txt).
-            prio_feedback(leadp, ++prog, kDecPrioDiv);
+            prio_feedback(leadp, ++prog, CYAES_DEC_RAGGED_DIV);
             pv[0] = shr1(c[0], carry);
 #pragma unroll
             for (int k = 1; k < R; k++)
@@ -245,7 +270,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
             for (int k = 0; k < R; k++) {
                 Ext we = re[k];
                 if constexpr (CYAES_BOUNDS_CHECK) we = ext(a.out + (we.lo - a.in), we.hi - we.lo);
-                if (valid[k]) ST16U(a.out + orow[k], we, pv[k]);
+                if (valid[k]) ST16U(regular ? gout + o32[k] : a.out + orow[k], we, pv[k]);
             }
             carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
         }

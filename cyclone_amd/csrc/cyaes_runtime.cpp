@@ -594,8 +594,15 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     // group from the launch's ticket counter, so the finer the groups the closer
     // the waves finish; static: >= 2), up to 64 (one holder lane each); small
     // payloads then share rows.  Sweeps in profiles/r01/ab_ragged_groups.txt, r04.
+    // Dynamic groups by default when the batch has too few payloads for
+    // 64-payload groups under the static split (fewer than 128 per wave of a
+    // full grid): its payloads are then long, and their lengths uneven (a
+    // relay stream of 0xFF00-B chunks and short tails: decrypt -25 % against
+    // the static split, profiles/r06/ab/mixed_env.txt); many short payloads
+    // (MTU packets) keep the static split (r04: the pool no faster there).
     const uint64_t slots = (uint64_t)std::max(1, ctx->num_cus) * (kDecThreads / 64);
-    const uint64_t per_wave = ctx->dec_dyn == 1 ? std::max<uint32_t>(1, ctx->dec_groups_per_wave) : 2;
+    const bool dyn = ctx->dec_dyn == 1 || (ctx->dec_dyn < 0 && npayloads < 64 * 2 * slots);
+    const uint64_t per_wave = dyn ? std::max<uint32_t>(1, ctx->dec_groups_per_wave) : 2;
     const uint64_t G = ctx->ragged_group ? ctx->ragged_group
                                          : std::min<uint64_t>(64, std::max<uint64_t>(1, npayloads / (per_wave * slots)));
     a.group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, G));
@@ -606,7 +613,7 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     // Groups [0, nstat) static (strided over the waves), the rest a dynamic pool
     // from per-XCD ticket pools with stealing (as the flat kernel's ranges).
     const uint64_t nwaves = (uint64_t)grid * (sh.threads / 64);
-    a.dyn = ctx->dec_dyn == 1 && a.nranges > nwaves;  // (off by default: no faster on relay streams, r04)
+    a.dyn = dyn && a.nranges > nwaves;
     if (a.dyn) {
         const uint64_t stat_per_wave = a.nranges * (100 - std::min<uint32_t>(ctx->dec_dyn_pct, 100)) / 100 / nwaves;
         a.nstat = (uint32_t)(stat_per_wave * nwaves);
@@ -1104,6 +1111,106 @@ int cyaes_gpu_duplex_uniform(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d
     x.e = ep.a;
     x.d = dp.a;
     CY_TRY(launch_duplex(x, ep.grid, s));
+    return note_key_use(ctx, te, s);
+}
+
+// Duplex of two relay streams (r06): the sender's stream
+// encrypted by 64-B lines while the receiver's is decrypted by the flat
+// kernel's strided rows, in one grid.  Same results as
+//   cyaes_gpu_encrypt_strided(enc stream, key row enc_key)
+//   cyaes_gpu_decrypt_strided(dec stream, key row dec_key)
+// in that order; whenever one half would not take those kernels (short or
+// unaligned streams, spans past 32-bit offsets, overlapping streams) it runs
+// as exactly those two calls.
+int cyaes_gpu_duplex_strided(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d_enc_out, uint64_t enc_first,
+                             uint64_t enc_stride, uint64_t enc_npayloads, uint32_t enc_payload_bytes, uint32_t enc_key,
+                             const uint8_t* d_dec_in, uint8_t* d_dec_out, uint64_t dec_first, uint64_t dec_stride,
+                             uint64_t dec_npayloads, uint32_t dec_payload_bytes, uint32_t dec_key, void* stream) {
+    if (!ctx) return CYAES_EINVAL;
+    const bool has_e = enc_npayloads && enc_payload_bytes, has_d = dec_npayloads && dec_payload_bytes;
+    auto half_ok = [&](const uint8_t* in, const uint8_t* out, uint64_t first, uint64_t stride, uint64_t n,
+                       uint32_t pb) {
+        return pb % 16 == 0 && first % 4 == 0 && stride % 4 == 0 && stride >= pb && ragged_args_ok(ctx, in, out, nullptr, nullptr) &&
+               n - 1 <= (UINT64_MAX - first - pb) / stride;
+    };
+    if (enc_payload_bytes % 16 || dec_payload_bytes % 16) return CYAES_EINVAL;
+    if (has_e && !half_ok(d_enc_in, d_enc_out, enc_first, enc_stride, enc_npayloads, enc_payload_bytes))
+        return CYAES_EINVAL;
+    if (has_d && !half_ok(d_dec_in, d_dec_out, dec_first, dec_stride, dec_npayloads, dec_payload_bytes))
+        return CYAES_EINVAL;
+    if ((has_e && enc_key >= ctx->nkeys) || (has_d && dec_key >= ctx->nkeys)) return CYAES_ERANGE;
+    if (!has_e && !has_d) return CYAES_OK;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t* te = ctx->d_keys + (uint64_t)enc_key * kSchedWords;
+    const uint32_t* td = ctx->d_keys + (uint64_t)dec_key * kSchedWords;
+    const uint64_t espan = has_e ? (enc_npayloads - 1) * enc_stride + enc_payload_bytes : 0;
+    const uint64_t dspan = has_d ? (dec_npayloads - 1) * dec_stride + dec_payload_bytes : 0;
+    auto sequential = [&]() -> int {
+        if (has_e) {  // (the strided entry points' own kernel choice, under the key row)
+            const int st = enc_stride == enc_payload_bytes && batch_args_ok(ctx, d_enc_in + enc_first, d_enc_out + enc_first, nullptr, nullptr)
+                               ? encrypt_common(ctx, d_enc_in + enc_first, d_enc_out + enc_first, nullptr, nullptr,
+                                                enc_npayloads, enc_payload_bytes, nullptr, 0, nullptr, nullptr, s, te, 1)
+                               : encrypt_common(ctx, d_enc_in, d_enc_out, nullptr, nullptr, enc_npayloads,
+                                                enc_payload_bytes, nullptr, 0, nullptr, nullptr, s, te, 1, enc_first,
+                                                enc_stride);
+            if (st) return st;
+        }
+        if (!has_d) return CYAES_OK;
+        if (dec_stride == dec_payload_bytes && batch_args_ok(ctx, d_dec_in + dec_first, d_dec_out + dec_first, nullptr, nullptr))
+            return decrypt_uniform(ctx, d_dec_in + dec_first, d_dec_out + dec_first, dec_npayloads, dec_payload_bytes,
+                                   nullptr, 0, nullptr, nullptr, s, td, 1);
+        if (dec_payload_bytes / 16 >= 64 && dspan <= 0xFFFFFFFFull && !ctx->strided_lists)
+            return decrypt_uniform(ctx, d_dec_in, d_dec_out, dec_npayloads, dec_payload_bytes, nullptr, 0, nullptr,
+                                   nullptr, s, td, 1, dec_first, dec_stride);
+        StreamScratch lists;
+        int st = lists.get(ctx, dec_npayloads * 12, s);
+        if (st) return st;
+        uint64_t* offs = static_cast<uint64_t*>(lists.p);
+        uint32_t* nb = reinterpret_cast<uint32_t*>(offs + dec_npayloads);
+        CY_TRY(launch_strided_lists(offs, nb, dec_first, dec_stride, dec_npayloads, dec_payload_bytes, s));
+        return decrypt_ragged(ctx, d_dec_in, d_dec_out, offs, nb, dec_npayloads, nullptr, 0, nullptr, nullptr, s, td, 1);
+    };
+    if (!has_e || !has_d || ctx->duplex_off) return sequential();
+    // The duplex form: the encrypt half's whole line groups by lines, its
+    // decrypt half by the flat strided rows; 16-B aligned back-to-back streams
+    // are uniform batches (cyaes_gpu_duplex_uniform's business).
+    const uint64_t nlines = enc_npayloads / kLinesGroup * kLinesGroup;
+    const bool e_lines = !ctx->enc_no_lines && enc_stride != enc_payload_bytes && nlines &&
+                         (nlines - 1) * enc_stride + enc_payload_bytes + enc_first + 64 <= 0xFFFFFFFFull &&
+                         !ragged_encrypt_is_quad(ctx, enc_npayloads);
+    const bool d_flat = dec_stride != dec_payload_bytes && dec_payload_bytes / 16 >= 64 && dspan <= 0xFFFFFFFFull &&
+                        !ctx->strided_lists;
+    if (!e_lines || !d_flat || overlaps(d_enc_out + enc_first, espan, d_dec_in + dec_first, dspan) ||
+        overlaps(d_enc_out + enc_first, espan, d_dec_out + dec_first, dspan) ||
+        overlaps(d_dec_out + dec_first, dspan, d_enc_in + enc_first, espan))
+        return sequential();
+    EncPlan ep;
+    int st = enc_plan(ctx, d_enc_in, d_enc_out, nullptr, nullptr, nlines, enc_payload_bytes, nullptr, 0, nullptr,
+                      nullptr, te, 1, enc_first, enc_stride, &ep);
+    if (st) return st;
+    const Shape sh = wave_shape(ctx, nlines / 64, kEncThreads);
+    const int grid = std::min(sh.grid, enc_grid_cap(ctx));
+    if (sh.threads != kDecThreads) return sequential();
+    // The rest of the encrypt stream (< 1,024 payloads) first, as the strided entry point runs it.
+    if (nlines < enc_npayloads) {
+        st = encrypt_common(ctx, d_enc_in, d_enc_out, nullptr, nullptr, enc_npayloads - nlines, enc_payload_bytes,
+                            nullptr, 0, nullptr, nullptr, s, te, 1, enc_first + nlines * enc_stride, enc_stride);
+        if (st) return st;
+    }
+    DecPlan dp;
+    st = dec_plan(ctx, d_dec_in, d_dec_out, dec_npayloads, dec_payload_bytes, nullptr, 0, nullptr, nullptr, s, td, 1,
+                  dec_first, dec_stride, (int)ctx->duplex_dyn_pct, grid, &dp);
+    if (st) return st;
+    if (!dp.a.dyn) {  // a decrypt too short for a pool: the two launches
+        CY_TRY(launch_encrypt_lines(ep.a, grid, kEncThreads, s));
+        CY_TRY(launch_decrypt_flat(dp.a, dp.grid, s));
+        return note_key_use(ctx, te, s);
+    }
+    DuplexArgs x;
+    x.e = ep.a;
+    x.d = dp.a;
+    CY_TRY(launch_duplex_lines(x, grid, s));
     return note_key_use(ctx, te, s);
 }
 

@@ -175,6 +175,24 @@ int cyaes_gpu_duplex_uniform(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d
                              uint32_t enc_payload_bytes, uint32_t enc_key, const uint8_t* d_dec_in, uint8_t* d_dec_out,
                              uint64_t dec_npayloads, uint32_t dec_payload_bytes, uint32_t dec_key, void* stream);
 
+/* Duplex of two relay streams (strided layout, as cyaes_gpu_{en,de}crypt_strided):
+ * the stream a relay end sends (encrypted, relay_local.cpp:206 /
+ * relay_server.cpp:472) and the one it receives (decrypted, relay_server.cpp:329
+ * / relay_local.cpp:365) in ONE launch.  Same results as
+ *   cyaes_gpu_encrypt_strided(enc stream, key row enc_key)
+ *   cyaes_gpu_decrypt_strided(dec stream, key row dec_key)
+ * in that order (unkeyed within each half, one key row each, no IV arrays).
+ * The encrypt half's whole 1,024-payload groups are read by 64-B lines, the
+ * decrypt half by the flat kernel's strided rows; streams those kernels do not
+ * take (short, unaligned, > 4 GiB spans, 16-B aligned back-to-back payloads)
+ * and overlapping streams run as the two calls.  Errors as the strided entry
+ * points; CYAES_ERANGE for a key row >= the number of keys set. */
+int cyaes_gpu_duplex_strided(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d_enc_out, uint64_t enc_first_offset,
+                             uint64_t enc_stride, uint64_t enc_npayloads, uint32_t enc_payload_bytes, uint32_t enc_key,
+                             const uint8_t* d_dec_in, uint8_t* d_dec_out, uint64_t dec_first_offset,
+                             uint64_t dec_stride, uint64_t dec_npayloads, uint32_t dec_payload_bytes, uint32_t dec_key,
+                             void* stream);
+
 /* ---- Host-resident uniform batches (PCIe-inclusive) ----------------------
  * The relay path starts and ends in host memory (socket buffers).  These
  * process npayloads uniform payloads that live in HOST memory: chunks of

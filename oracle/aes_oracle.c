@@ -328,6 +328,53 @@ int cyo_batch(int decrypt, const cyo_key* keys, uint32_t payloads_per_key, const
     return 0;
 }
 
+/* Ragged relay stream: payload p = bytes [offsets[p], offsets[p] + nbytes[p])
+ * of buf (in place), one independent chain from DefaultIV per payload under
+ * one key -- the relay's per-packet calls on a received / sent stream
+ * (relay_server.cpp:329 decrypt(buf, buf, packet_size - 8), relay_local.cpp:206
+ * encrypt(buf, buf, round16(size))), payloads split over nthreads threads. */
+typedef struct ragged_job {
+    int decrypt;
+    const cyo_key* key;
+    uint8_t* buf;
+    const uint64_t* offsets;
+    const uint32_t* nbytes;
+    uint64_t p_begin, p_end;
+    int rc;
+} ragged_job;
+
+static void* ragged_worker(void* arg) {
+    ragged_job* j = (ragged_job*)arg;
+    for (uint64_t p = j->p_begin; p < j->p_end; p++) {
+        uint8_t* q = j->buf + j->offsets[p];
+        const int rc = j->decrypt ? cyo_decrypt(j->key, q, q, j->nbytes[p], NULL)
+                                  : cyo_encrypt(j->key, q, q, j->nbytes[p], NULL);
+        if (rc) j->rc = rc;
+    }
+    return NULL;
+}
+
+int cyo_batch_ragged(int decrypt, const cyo_key* key, uint8_t* buf, const uint64_t* offsets,
+                     const uint32_t* nbytes, uint64_t npayloads, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if ((uint64_t)nthreads > npayloads) nthreads = npayloads ? (int)npayloads : 1;
+    ragged_job* jobs = (ragged_job*)calloc((size_t)nthreads, sizeof(ragged_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    if (!jobs || !th) { free(jobs); free(th); return -1; }
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (ragged_job){decrypt, key, buf, offsets, nbytes, npayloads * (uint64_t)t / (uint64_t)nthreads,
+                               npayloads * (uint64_t)(t + 1) / (uint64_t)nthreads, 0};
+    }
+    for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, ragged_worker, &jobs[t]);
+    ragged_worker(&jobs[0]);
+    int rc = 0;
+    for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+    for (int t = 0; t < nthreads; t++) if (jobs[t].rc) rc = jobs[t].rc;
+    free(jobs);
+    free(th);
+    return rc;
+}
+
 /* ---- Adler-32 (cyr_adler32.cpp:66-133), restated step for step ----------
  * BASE 65521 (:12), NMAX 5552 (:13): sums of NMAX bytes fit 32 bits before a
  * modulo.  Edge rules: NULL or len 0 -> INITIAL_ADLER (:72-73); len 1 uses

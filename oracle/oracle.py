@@ -48,6 +48,8 @@ def lib():
         L.cyo_session_key.argtypes = [ctypes.c_uint64, ctypes.c_uint64, _u8p]
         L.cyo_batch.argtypes = [ctypes.c_int, ctypes.POINTER(OracleKey), ctypes.c_uint32, _u8p, _u8p,
                                 ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int]
+        L.cyo_batch_ragged.argtypes = [ctypes.c_int, ctypes.POINTER(OracleKey), ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -136,6 +138,22 @@ def batch(decrypt, keys, payloads_per_key, data, payload_bytes, nthreads=1):
     if rc != 0:
         raise ValueError("oracle batch rejected arguments")
     return out
+
+
+def batch_ragged(decrypt, key, buf, offsets, nbytes, nthreads=1):
+    """Relay stream in place: payload p = buf[offsets[p] : offsets[p] + nbytes[p]],
+    each an independent chain from DefaultIV under one key (cyo_batch_ragged).
+    buf: writable contiguous uint8 numpy array, modified in place."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    nbytes = np.ascontiguousarray(nbytes, dtype=np.uint32)
+    if offsets.size != nbytes.size or (offsets.size and int((offsets + nbytes).max()) > buf.size):
+        raise ValueError("payload outside the buffer")
+    k = key_expand(key)
+    rc = lib().cyo_batch_ragged(1 if decrypt else 0, ctypes.byref(k), buf.ctypes.data, offsets.ctypes.data,
+                                nbytes.ctypes.data, offsets.size, nthreads)
+    if rc != 0:
+        raise ValueError("oracle ragged batch rejected arguments")
+    return buf
 
 
 def _splitmix64(x):

@@ -1051,6 +1051,79 @@ def test_duplex_sweep(torch, seed):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("shape", ["relay", "relay_rest", "relay_big", "short", "aligned", "lists", "overlap",
+                                   "empty_dec", "off", "relay_pool"])
+def test_duplex_strided_matches_two_strided_calls(torch, shape):
+    """cyaes_gpu_duplex_strided (two relay streams, one launch: relay_server.cpp
+    :472 encrypts the sent stream while :329 decrypts the received one) against
+    cyaes_gpu_encrypt_strided + cyaes_gpu_decrypt_strided of reference contexts
+    (one per key row), bit-exact, bytes between payloads untouched, in place:
+    relay packets (payload at offset 12, stride 1,484) with whole 1,024-payload
+    line groups and a rest; >= 256-block payloads; shapes that fall back to the
+    two calls (short streams, 16-B aligned back-to-back payloads, < 64-block
+    decrypt payloads that take the ragged kernel, overlapping streams, an empty
+    half, CYAES_DUPLEX=0); the decrypt's pool share forced to 100 %."""
+    keys = [K0, oracle.session_key(5), oracle.session_key(6)]
+    env = {"off": {"CYAES_DUPLEX": "0"}, "relay_pool": {"CYAES_DUPLEX_DYN_PCT": "100"}}.get(shape, {})
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        c = ca.GpuContext(0)
+    finally:
+        _restore(old)
+    c.set_keys(b"".join(keys))
+    ref = [ca.GpuContext(0) for _ in keys]
+    for r, k in zip(ref, keys):
+        r.set_keys(k)
+    # (first, stride, n, payload bytes) per half
+    e, d = {"relay": ((12, 1484, 1 << 20, 1472), (12, 1484, 300000, 1472)),
+            "relay_rest": ((12, 1484, 262144 + 437, 1472), (44, 1500, 200003, 1472)),
+            "relay_big": ((12, 4108, 262144, 4096), (12, 65548, 3000, 65536)),
+            "short": ((12, 1484, 900, 1472), (12, 1484, 100000, 1472)),
+            "aligned": ((0, 1472, 300000, 1472), (0, 2048, 300000, 2048)),
+            "lists": ((12, 1484, 262144, 1472), (12, 524, 300000, 512)),
+            "overlap": ((12, 1484, 262144, 1472), (12, 1484, 262144, 1472)),
+            "empty_dec": ((12, 1484, 262144, 1472), (12, 1484, 0, 1472)),
+            "off": ((12, 1484, 262144, 1472), (12, 1484, 300000, 1472)),
+            "relay_pool": ((12, 1484, 1 << 20, 1472), (12, 1484, 1 << 20, 1472))}[shape]
+    ek, dk = (1, 2) if shape in ("relay", "relay_big", "relay_rest") else (0, 0)
+
+    def span(h):
+        f, s, n, pb = h
+        return ((f + (n - 1) * s + pb + 16) // 16 * 16) if n else 16
+    e_buf = empty(torch, span(e))
+    d_buf = e_buf if shape == "overlap" else empty(torch, span(d))
+    c.fill_synthetic(e_buf, 3, e_buf.numel() // 16, 16, oracle.PLAINTEXT_SEED)
+    if shape != "overlap":
+        c.fill_synthetic(d_buf, 9, d_buf.numel() // 16, 16, oracle.PLAINTEXT_SEED)
+    want_e, want_d = e_buf.clone(), (e_buf.clone() if shape == "overlap" else d_buf.clone())
+    if shape == "overlap":  # encrypt-then-decrypt order on one buffer
+        ref[ek].encrypt_strided(want_e, want_e, *e)
+        want_d = want_e
+        ref[dk].decrypt_strided(want_d, want_d, *d)
+    else:
+        ref[ek].encrypt_strided(want_e, want_e, *e)
+        if d[2]:
+            ref[dk].decrypt_strided(want_d, want_d, *d)
+    c.duplex_strided(e_buf, e_buf, *e, d_buf, d_buf, *d, enc_key=ek, dec_key=dk)
+    assert torch.equal(e_buf, want_e), (shape, e)
+    assert torch.equal(d_buf, want_d), (shape, d)
+    if shape != "overlap":  # the sent stream decrypts back
+        ref[ek].decrypt_strided(e_buf, e_buf, *e)
+        chk = empty(torch, span(e))
+        c.fill_synthetic(chk, 3, chk.numel() // 16, 16, oracle.PLAINTEXT_SEED)
+        assert torch.equal(e_buf, chk)
+    with pytest.raises(ca.CyaesError):
+        c.duplex_strided(e_buf, e_buf, 2, 1484, 4, 1472, d_buf, d_buf, 12, 1484, 4, 1472)  # first % 4
+    with pytest.raises(ca.CyaesError):
+        c.duplex_strided(e_buf, e_buf, 12, 1484, 4, 1472, d_buf, d_buf, 12, 1484, 4, 1472, dec_key=3)
+    assert c.check() == ca.CYAES_OK
+    for r in ref:
+        r.close()
+    c.close()
+    torch.cuda.empty_cache()
+
+
 def test_dropin_size_zero_and_pieces():
     """The drop-in's argument rules: size 0 is a no-op whatever the
     pointers (the reference's loop never runs, cyr_rijndael.cpp:600), and a call

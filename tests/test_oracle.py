@@ -220,3 +220,45 @@ def test_adler32_oracle_random_split_and_zlib():
         assert oracle.adler32(start, buf) == zlib.adler32(buf, start)
     # the reference's own rule differs from zlib for len == 0
     assert oracle.adler32(0xdeadbeef, b"") == 1 and zlib.adler32(b"", 0xdeadbeef) == 0xdeadbeef
+
+
+def test_ragged_relay_batch_matches_per_packet_calls():
+    """cyo_batch_ragged (the relay stream restatement): each payload of a
+    ragged in-place stream equals one Rijndael::encrypt(buf, buf, size) call
+    from DefaultIV (relay_local.cpp:206), payloads at 4-B phases, sizes 0 to
+    0xFF00; decrypt restores the stream; bytes between payloads untouched."""
+    rng = np.random.default_rng(11)
+    key = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+    sizes = np.array([0, 16, 0xFF00, 1472, 32, 4080, 65264, 16 * 7], dtype=np.uint32)
+    pkt = sizes.astype(np.uint64) + 12
+    offsets = (np.cumsum(pkt) - pkt + 12).astype(np.uint64)
+    buf = rng.integers(0, 256, int(pkt.sum()) + 16, dtype=np.uint8)
+    ref = buf.copy()
+    oracle.batch_ragged(False, key, buf, offsets, sizes, nthreads=3)
+    aes = oracle.Rijndael(key)
+    mask = np.ones(buf.size, dtype=bool)
+    for o, n in zip(offsets.tolist(), sizes.tolist()):
+        want = bytes(aes.encrypt(ref[o:o + n].tobytes(), None, n, None)) if n else b""
+        assert bytes(buf[o:o + n]) == want
+        mask[o:o + n] = False
+    assert np.array_equal(buf[mask], ref[mask])
+    oracle.batch_ragged(True, key, buf, offsets, sizes, nthreads=2)
+    assert np.array_equal(buf, ref)
+
+
+def test_mixed_relay_stream_layout_is_the_golden_one():
+    """bench.py's relay_stream.mixed regenerates the layout its golden digests
+    (tests/golden/relay_mixed.json) were computed on: same packets, payload
+    bytes, stream size and offset / size lists (hash)."""
+    import json
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    g = json.load(open(os.path.join(root, "tests", "golden", "relay_mixed.json")))
+    offsets, nbytes, alloc = bench.mixed_stream_layout(g["chunk_bytes"])
+    assert (int(offsets.size), int(nbytes.sum()), alloc) == (g["packets"], g["payload_bytes"], g["stream_bytes"])
+    assert hashlib.sha256(offsets.tobytes() + nbytes.tobytes()).hexdigest()[:16] == g["layout_sha256_16"]
+    assert int(nbytes.max()) == bench.RELAY_MAX_CHUNK and int((nbytes % 16).max()) == 0
+    assert int(offsets[0]) == 12 and np.all(offsets[1:] == offsets[:-1] + nbytes[:-1].astype(np.uint64) + 12)
