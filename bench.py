@@ -239,31 +239,41 @@ def cpu_baseline(cfg_name, npay, pb, ppk, d_ct, torch, sample=0):
     keys = [bytes(range(16))] if not ppk else [session_keys(sample // ppk + 1)[16 * s:16 * s + 16]
                                               for s in range(sample // ppk + 1)]
     pt = oracle.synthetic(0, sample, pb)
+    # A small config (A: 4 MiB) is timed over repeats of the whole batch, at
+    # least 256 MiB of payload per direction, so thread start-up does not dominate.
+    reps = max(1, -(-(256 << 20) // (sample * pb)))
     t0 = time.perf_counter()
-    ct = oracle.batch(False, keys, ppk, pt, pb, nthreads=threads)
+    for _ in range(reps):
+        ct = oracle.batch(False, keys, ppk, pt, pb, nthreads=threads)
     t1 = time.perf_counter()
-    rt = oracle.batch(True, keys, ppk, ct, pb, nthreads=threads)
+    for _ in range(reps):
+        rt = oracle.batch(True, keys, ppk, ct, pb, nthreads=threads)
     t2 = time.perf_counter()
     # single-core figure on a smaller slice
     s1 = max(1, min(sample, (256 << 20) // pb))
+    reps1 = max(1, -(-(32 << 20) // (s1 * pb)))
     t3 = time.perf_counter()
-    ct1 = oracle.batch(False, keys, ppk, pt[:s1 * pb], pb, nthreads=1)
+    for _ in range(reps1):
+        ct1 = oracle.batch(False, keys, ppk, pt[:s1 * pb], pb, nthreads=1)
     t4 = time.perf_counter()
-    oracle.batch(True, keys, ppk, ct1, pb, nthreads=1)
+    for _ in range(reps1):
+        oracle.batch(True, keys, ppk, ct1, pb, nthreads=1)
     t5 = time.perf_counter()
     torch.cuda.synchronize()
     gpu_sample = d_ct[: sample * pb].cpu().numpy()
     exact = bool(np.array_equal(gpu_sample, ct)) and bool(np.array_equal(rt, pt))
     gib = float(1 << 30)
     return dict({
-        "value": round(2 * sample * pb / (t2 - t0) / gib, 4),
+        "value": round(2 * reps * sample * pb / (t2 - t0) / gib, 4),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
         "sample": "config %s: first %d payloads x %d B (%.2f GiB), encrypt then decrypt, %d threads = the usable "
-                  "host cores (one Rijndael key schedule per thread, as relay's work threads, relay_local.cpp:475); "
-                  "oracle/aes_oracle.c" % (cfg_name, sample, pb, sample * pb / gib, threads),
-        "single_core": round(2 * s1 * pb / ((t4 - t3) + (t5 - t4)) / gib, 4),
+                  "host cores (one Rijndael key schedule per thread, as relay's work threads, relay_local.cpp:475)%s; "
+                  "oracle/aes_oracle.c" % (cfg_name, sample, pb, sample * pb / gib, threads,
+                                           ", the whole batch %d times per direction" % reps if reps > 1 else ""),
+        "single_core": round(2 * reps1 * s1 * pb / ((t4 - t3) + (t5 - t4)) / gib, 4),
+        "repeats": reps,
         "seconds": round(t2 - t0, 3),
         "matches_gpu": exact,
     }, **facts)
