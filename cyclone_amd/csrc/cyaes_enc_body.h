@@ -86,7 +86,12 @@ __device__ __forceinline__ void enc_body(const EncArgs& a, const char* lds, uint
     const Ext iv_in_e = iv_ext(a.iv_in, a.npayloads), iv_out_e = iv_ext(a.iv_out, a.npayloads);
     const uint32_t R = RUNS ? a.run : 1u;  // payloads per work item
     const uint32_t bpp = a.payload_bytes >> 4;
-    const uint64_t nwork = RUNS ? (a.npayloads + R - 1) / R : a.npayloads;
+    // RAGGED with a.rest: the waves k_encrypt_rag_lines handed back (their
+    // count at rest[0], written by it earlier on the stream), each the 64
+    // payloads 16 apart of a 1,024-payload group that the line walk gives a wave.
+    const bool listed = RAGGED && a.rest != nullptr;
+    const uint64_t nwork = listed ? 64ull * __builtin_amdgcn_readfirstlane(LD4(a.rest, ext(a.rest, 4)))
+                                  : RUNS ? (a.npayloads + R - 1) / R : a.npayloads;
     uint32_t ek[44];
     // One schedule per wave, loaded before the loop: the whole batch's, or
     // (SESS) the wave's session's, from its scalar position.  A SESS grid covers
@@ -98,8 +103,13 @@ __device__ __forceinline__ void enc_body(const EncArgs& a, const char* lds, uint
     else if (!KEYED) load_sched(a.keys, 0, 0, ek);
 
     for (uint64_t wbase = wbase0; wbase < nwork; wbase += wstride) {
-        const uint64_t w = wbase + lane;
+        uint64_t w = wbase + lane;
         const bool active = w < nwork;
+        if (listed) {
+            const uint32_t gw = __builtin_amdgcn_readfirstlane(
+                LD4(a.rest + 1 + (wbase >> 6), ext(a.rest, 4 + 4 * (nwork >> 6))));
+            w = (uint64_t)(gw >> 4) * 1024u + (gw & 15u) + 16u * lane;
+        }
         const uint64_t p = RUNS ? w * R : w;  // (first) payload of the work item
         uint64_t off;
         uint32_t nb;

@@ -35,7 +35,24 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_lines(EncArgs a) {
 }
 
 
+// Ragged batches' whole 1,024-payload groups by lines (cyaes_lines_body.h,
+// rag_lines_walk); the waves it hands back go to k_encrypt<RAGGED> next.
+__global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_rag_lines(EncArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
+    fill_enc_image(lds_words, a.tables);
+    __shared__ uint32_t lead;  // prio_feedback
+    if (threadIdx.x == 0) lead = 0;
+    __syncthreads();
+    CLOCK_PROBE(0);
+    rag_lines_walk(a, reinterpret_cast<const char*>(lds_words), &lead);
+}
+
 }  // namespace
+
+hipError_t launch_encrypt_rag_lines(const EncArgs& a, int grid, int threads, hipStream_t stream) {
+    hipLaunchKernelGGL(k_encrypt_rag_lines, dim3(grid), dim3(threads), 0, stream, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_encrypt_lines(const EncArgs& a, int grid, int threads, hipStream_t stream) {
     hipLaunchKernelGGL(k_encrypt_lines, dim3(grid), dim3(threads), 0, stream, a);

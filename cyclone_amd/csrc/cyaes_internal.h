@@ -107,6 +107,10 @@ struct EncArgs {
     uint32_t sess_payloads;  // uniform lane kernel: payloads_per_key when every wave lies in one session (SESS), else 0
     uint64_t off0, stride;   // ragged kernels, stride != 0: payload p at byte off0 + p * stride, payload_bytes each
                              // (cyaes_gpu_encrypt_strided; offsets / nbytes are not read)
+    // Ragged batches by lines (r06): rest[0] counts the line-walk waves
+    // (1,024-payload-group wave indices, rest[1..]) the line kernel handed back;
+    // the ragged lane kernel, given rest, walks exactly those waves' payloads.
+    uint32_t* rest;
 };
 
 // Per-launch decrypt scratch (DecArgs.work): words kWorkCtrOff + 64 * x are
@@ -171,6 +175,9 @@ hipError_t launch_encrypt(const EncArgs& a, int grid, int threads, hipStream_t s
 // Strided, unkeyed, no IV arrays, npayloads a multiple of kLinesGroup (k_encrypt_lines).
 constexpr uint64_t kLinesGroup = 1024;
 hipError_t launch_encrypt_lines(const EncArgs& a, int grid, int threads, hipStream_t stream);
+// Ragged (lists), unkeyed, no IV arrays, npayloads a multiple of kLinesGroup,
+// a.rest zeroed at [0] and room for npayloads / 64 wave indices after it.
+hipError_t launch_encrypt_rag_lines(const EncArgs& a, int grid, int threads, hipStream_t stream);
 // Four lanes per chain (latency-bound batches; threads a multiple of 64).
 hipError_t launch_encrypt_quad(const EncArgs& a, int grid, int threads, hipStream_t stream);
 hipError_t launch_decrypt_flat(const DecArgs& a, int grid, hipStream_t stream);

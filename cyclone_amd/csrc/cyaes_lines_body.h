@@ -188,5 +188,124 @@ __device__ __forceinline__ void lines_walk(const EncArgs& a, const char* lds, ui
     }
 }
 
+// Ragged (list) batches by lines (r06): k_encrypt_lines
+// over the first whole 1,024-payload groups of an unkeyed ragged batch without
+// IV arrays.  Wave g takes the payloads lines_walk gives it (16 apart: a relay
+// stream's waves are then phase-uniform whatever its packet size), loads its
+// 64 offsets and sizes, and walks them exactly as lines_walk does when they
+// share one line phase and one length and lie within 4 GiB - 64 B of the
+// lowest of them, with the group members' positions (VGPRs, 32-bit) in place of
+// the stride.  Any other wave appends its index to a.rest (count at [0]) and
+// leaves its payloads to the ragged lane kernel, which walks that list next
+// (enc_body, a.rest).  No prefetch of the next item's first chunk (the
+// members' positions of two items at once did not fit the registers).
+__device__ __forceinline__ void rag_lines_walk(const EncArgs& a, const char* lds, uint32_t* lead) {
+    uint32_t prog = 0;
+    const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t mem = lane >> 4;
+    uint32_t ek[44];
+    load_sched(a.keys, 0, 0, ek);
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb, gwaves = a.npayloads / 64u;
+    const uintptr_t in0 = reinterpret_cast<uintptr_t>(a.in);
+    for (uint64_t g = (uint64_t)blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); g < gwaves;
+         g += nwaves) {
+        const uint64_t pl = (g >> 4) * 1024u + (g & 15u) + 16u * lane;  // this lane's payload
+        const uint64_t off = LD8(a.offsets + pl, ext(a.offsets, 8 * a.npayloads));
+        const uint32_t nb = LD4(a.nbytes + pl, ext(a.nbytes, 4 * a.npayloads)) >> 4;
+        const uint32_t nb0 = __builtin_amdgcn_readfirstlane(nb);
+        const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(in0 + off) & 63u);
+        uint64_t wlo = off;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t o2 = (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(wlo >> 32), d) << 32 |
+                                (uint32_t)__shfl_xor((int)(uint32_t)wlo, d);
+            wlo = min(wlo, o2);
+        }
+        wlo = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wlo >> 32)) << 32 |
+              __builtin_amdgcn_readfirstlane((uint32_t)wlo);
+        const bool ok = nb0 > 0 && __ballot(nb != nb0 || ((uint32_t)(in0 + off) & 63u) != m ||
+                                            off - wlo + 16ull * nb0 + 128u >= (1ull << 32)) == 0;
+        if (!ok) {  // to the lane kernel
+            if (lane == 0) {
+                const uint32_t i = atomicAdd(a.rest, 1u);
+                a.rest[1 + i] = (uint32_t)g;
+            }
+            continue;
+        }
+        // base: the lowest payload's first line (may precede a.in by < 64 B, inside its line)
+        const uint8_t* base = a.in + (wlo - m);
+        uint8_t* obase = a.out + (wlo - m);
+        uint32_t mrel[4];  // the group members' payloads (lanes k + 16 q): their first lines from base
+#pragma unroll
+        for (int q = 0; q < 4; q++) mrel[q] = (uint32_t)__shfl((int)(uint32_t)(off - wlo), (int)((lane & 15u) + 16u * q));
+        const uint32_t s = m >> 2;
+        const uint32_t e = (s + 3u) & 3u, j0 = (s + 3u) >> 2;
+        const uint32_t nlines = (m + 16u * nb0 + 63u) >> 6;
+        const uint32_t nchunks = (nb0 - 1u + j0) / 8u + 1u;
+        auto load_chunk = [&](uint4 (&v)[8], uint32_t t) {
+            const uint32_t l1 = min(2u * t + 1u, nlines - 1u) - 2u * t;  // 1, or 0 past the last line
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t lo64 = (j >> 2) ? 64u * l1 : 0u;
+                v[j] = LD16(base + (mrel[j & 3] + 128u * t + lo64 + 16u * mem), ext(base + mrel[j & 3], 64ull * nlines));
+            }
+        };
+        uint4 b[8];
+        load_chunk(b, 0);
+        transpose4(b), transpose4(b + 4);
+        uint32_t c0 = 0, c1 = 0, c2 = 0;
+        uint4 c = default_iv();
+        for (uint32_t t = 0; t < nchunks; t++) {
+            const bool more = t + 1 < nchunks;
+            const uint32_t jlo = t == 0 ? j0 : 0u;
+            const uint32_t jhi = min(8u, nb0 + j0 - 8u * t);
+            uint4 o[8];
+            auto cut = [&](auto et) {
+                constexpr int E = decltype(et)::value;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int K = E - 3 + 4 * j;
+                    o[j] = make_uint4(wdw_rt(b, c0, c1, c2, K), wdw_rt(b, c0, c1, c2, K + 1),
+                                      wdw_rt(b, c0, c1, c2, K + 2), wdw_rt(b, c0, c1, c2, K + 3));
+                }
+            };
+            if (e == 3) cut(std::integral_constant<int, 3>{});
+            else if (e == 2) cut(std::integral_constant<int, 2>{});
+            else if (e == 1) cut(std::integral_constant<int, 1>{});
+            else cut(std::integral_constant<int, 0>{});
+            c0 = b[7].y, c1 = b[7].z, c2 = b[7].w;
+            uint4 bn[8];
+            if (more) load_chunk(bn, t + 1);
+            prio_feedback(lead, ++prog, kEncPrioDiv);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                if ((uint32_t)j >= jlo && (uint32_t)j < jhi) {
+                    uint32_t s0 = xor3(c.x, o[j].x, ek[0]), s1 = xor3(c.y, o[j].y, ek[1]);
+                    uint32_t s2 = xor3(c.z, o[j].z, ek[2]), s3 = xor3(c.w, o[j].w, ek[3]);
+                    enc_block(lds, lo, ek, s0, s1, s2, s3);
+                    c = make_uint4(s0, s1, s2, s3);
+                    o[j] = c;
+                }
+            }
+            transpose4(o), transpose4(o + 4);
+            const uint32_t soff = m + 16u * (8u * t - j0 + mem);  // (32-bit: wraps below 0 before j0 in chunk 0)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t sl = mem + 4u * (uint32_t)(j >> 2);
+                if (sl >= jlo && sl < jhi)
+                    ST16U(obase + (mrel[j & 3] + soff + 64u * (uint32_t)(j >> 2)),
+                          ext(obase + mrel[j & 3] + m, 16ull * nb0), o[j]);
+            }
+            if (more) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) b[j] = bn[j];
+                transpose4(b), transpose4(b + 4);
+            }
+        }
+    }
+}
+
 }  // namespace
 }  // namespace cyaes

@@ -25,6 +25,7 @@ struct cyaes_gpu {
     uint32_t enc_run = 0;       // env CYAES_ENC_RUN: payloads per lane run of the uniform encrypt (0 = auto; tests, A/B)
     bool enc_no_sess = false;   // env CYAES_ENC_NO_SESS=1: keyed uniform encrypt always by waterfall (tests, A/B)
     bool enc_no_lines = false;  // env CYAES_ENC_LINES=0: strided encrypts without k_encrypt_lines (tests, A/B)
+    bool enc_no_rag_lines = false;  // env CYAES_ENC_RAG_LINES=0: ragged encrypts without k_encrypt_rag_lines (tests, A/B)
     int lines_grid = 0;         // env CYAES_LINES_GRID: cap on k_encrypt_lines' grid (tests: several items per wave)
     int dec_dyn = -1;           // env CYAES_DEC_DYN: 1 / 0 force the dynamic decrypt pool on / off; -1: long launches only
     uint32_t dec_range_steps = kDecRangeSteps;  // env CYAES_DEC_RANGE_STEPS: steps per dynamic flat-decrypt range
@@ -265,6 +266,8 @@ int enc_plan(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* of
     return CYAES_OK;
 }
 
+int encrypt_rag_lines(cyaes_gpu* ctx, const EncArgs& a, uint64_t nrag, hipStream_t stream);
+
 int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
                    uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk,
                    const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream, const uint32_t* table = nullptr,
@@ -290,6 +293,16 @@ int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
         if (st || nlines_pay == npayloads) return st;
         return encrypt_common(ctx, in, out, nullptr, nullptr, npayloads - nlines_pay, payload_bytes, nullptr, 0,
                               nullptr, nullptr, stream, table, table_keys, off0 + nlines_pay * stride, stride);
+    }
+    // A ragged (list) batch for the lane kernel, unkeyed and without IV arrays:
+    // its whole 1,024-payload groups by lines first (encrypt_rag_lines).
+    const uint64_t nrag = npayloads / kLinesGroup * kLinesGroup;
+    if (offsets && !stride && !key_idx && !ppk && !iv_in && !iv_out && !plan.quad && nrag && !ctx->enc_no_lines &&
+        !ctx->enc_no_rag_lines) {
+        st = encrypt_rag_lines(ctx, plan.a, nrag, stream);
+        if (st || nrag == npayloads) return st;
+        return encrypt_common(ctx, in, out, offsets + nrag, nbytes + nrag, npayloads - nrag, payload_bytes, nullptr, 0,
+                              nullptr, nullptr, stream, table, table_keys);
     }
     if (plan.quad) CY_TRY(launch_encrypt_quad(plan.a, plan.grid, plan.threads, stream));
     else CY_TRY(launch_encrypt(plan.a, plan.grid, plan.threads, stream));
@@ -425,6 +438,25 @@ struct StreamScratch {
         b.in_use = !b.pending;
     }
 };
+
+// The whole 1,024-payload groups [0, nrag) of a ragged batch (unkeyed, no IV
+// arrays; the plan of the lane kernel in `a`): k_encrypt_rag_lines walks by
+// lines every wave whose payloads share a line phase and a length and hands
+// the others back through a device list, which the lane kernel then walks.
+int encrypt_rag_lines(cyaes_gpu* ctx, const EncArgs& a, uint64_t nrag, hipStream_t stream) {
+    StreamScratch rest;
+    int st = rest.get(ctx, 4 * (1 + nrag / 64), stream);
+    if (st) return st;
+    CY_TRY(hipMemsetAsync(rest.p, 0, 4, stream));
+    EncArgs la = a;
+    la.npayloads = nrag;
+    la.rest = static_cast<uint32_t*>(rest.p);
+    const Shape sh = wave_shape(ctx, nrag / 64, kEncThreads);
+    const int grid = std::min(sh.grid, enc_grid_cap(ctx));
+    CY_TRY(launch_encrypt_rag_lines(la, grid, sh.threads, stream));
+    CY_TRY(launch_encrypt(la, grid, sh.threads, stream));  // the waves handed back (none for a relay stream)
+    return note_key_use(ctx, la.keys.table, stream);
+}
 
 // d_iv_in == d_iv_out on a block-parallel decrypt: a payload's last block may
 // be written before its first block reads the IV, so read from a copy.
@@ -705,6 +737,7 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* v = getenv("CYAES_ENC_NO_SESS")) ctx->enc_no_sess = atoi(v) != 0;
     if (const char* v = getenv("CYAES_ENC_LINES")) ctx->enc_no_lines = atoi(v) == 0;
     if (const char* v = getenv("CYAES_LINES_GRID")) ctx->lines_grid = atoi(v);
+    if (const char* v = getenv("CYAES_ENC_RAG_LINES")) ctx->enc_no_rag_lines = atoi(v) == 0;
     if (const char* v = getenv("CYAES_DEC_DYN")) ctx->dec_dyn = atoi(v) != 0 ? 1 : 0;
     if (const char* v = getenv("CYAES_DEC_RANGE_STEPS")) ctx->dec_range_steps = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_DEC_GROUPS_PER_WAVE")) ctx->dec_groups_per_wave = (uint32_t)strtoul(v, nullptr, 10);

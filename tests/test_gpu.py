@@ -1124,6 +1124,83 @@ def test_duplex_strided_matches_two_strided_calls(torch, shape):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("layout", ["relay_inplace", "relay_out", "gaps", "half_regular", "sizes", "rest_and_empty"])
+def test_ragged_encrypt_by_lines(torch, layout):
+    """Ragged encrypts through k_encrypt_rag_lines: waves
+    whose 64 payloads (16 apart in a 1,024-payload group) share a line phase
+    and a length walk aligned lines; every other wave is handed back to the
+    ragged lane kernel through the device list; the rest past the last whole
+    group runs as its own batch.  Against a context with the line walk off
+    (CYAES_ENC_RAG_LINES=0), bytes outside the payloads untouched, the relay
+    stream's first 2,048 payloads also against the oracle, and decrypted back.
+    relay_local.cpp:206 encrypts each packet's payload in place."""
+    n = 131072 + (437 if layout == "rest_and_empty" else 0)
+    rng = np.random.default_rng(77)
+    pb = 1472
+    if layout in ("relay_inplace", "relay_out"):
+        sizes = np.full(n, pb, np.uint32)
+        gaps = np.full(n, 12, np.uint64)
+    elif layout == "gaps":
+        sizes = np.full(n, pb, np.uint32)
+        gaps = 12 + 4 * rng.integers(0, 3, n).astype(np.uint64)
+    elif layout == "half_regular":  # regular groups, then groups with random gaps
+        sizes = np.full(n, pb, np.uint32)
+        gaps = np.full(n, 12, np.uint64)
+        gaps[n // 2:] += (4 * rng.integers(0, 3, n - n // 2)).astype(np.uint64)
+    elif layout == "sizes":  # one phase pattern, lengths that differ inside some waves
+        sizes = np.full(n, pb, np.uint32)
+        sizes[rng.integers(0, n, 300)] = 16 * rng.integers(1, 200, 300)
+        gaps = np.full(n, 12, np.uint64)
+    else:
+        sizes = np.full(n, pb, np.uint32)
+        sizes[rng.integers(0, n, 50)] = 0
+        gaps = np.full(n, 12, np.uint64)
+    pkt = gaps + sizes.astype(np.uint64)
+    offsets = (np.cumsum(pkt) - sizes.astype(np.uint64)).astype(np.uint64)
+    total = int(offsets[-1] + sizes[-1]) + 64
+    old = {"CYAES_ENC_RAG_LINES": os.environ.get("CYAES_ENC_RAG_LINES")}
+    os.environ["CYAES_ENC_RAG_LINES"] = "0"
+    try:
+        ref = ca.GpuContext(0)
+    finally:
+        _restore(old)
+    c = ca.GpuContext(0)
+    c.set_keys(K0)
+    ref.set_keys(K0)
+    buf = empty(torch, (total + 15) // 16 * 16)
+    c.fill_synthetic(buf, 0, buf.numel() // 16, 16, oracle.PLAINTEXT_SEED)
+    d_off, d_nb = dev(torch, offsets), dev(torch, sizes)
+    want = buf.clone()
+    ref.encrypt_ragged(want, want, d_off, d_nb, n)
+    if layout == "relay_out":
+        out = torch.zeros_like(buf)
+        want_out = torch.zeros_like(buf)
+        ref.encrypt_ragged(buf, want_out, d_off, d_nb, n)
+        c.encrypt_ragged(buf, out, d_off, d_nb, n)
+        assert torch.equal(out, want_out)
+    else:
+        src = buf.clone()
+        c.encrypt_ragged(buf, buf, d_off, d_nb, n)
+        assert torch.equal(buf, want), layout
+        if layout == "relay_inplace":  # synthetic payloads: the oracle on a prefix, then back
+            view = buf[:n * 1484].view(n, 1484)[:, 12:12 + pb]
+            pt_b = empty(torch, n * pb)
+            c.fill_synthetic(pt_b, 0, n, pb, oracle.PLAINTEXT_SEED)
+            view.copy_(pt_b.view(n, pb))
+            c.encrypt_ragged(buf, buf, d_off, d_nb, n)
+            ct = view.contiguous().reshape(-1)
+            want_b = oracle.batch(False, [K0], 0, pt_b.cpu().numpy()[:2048 * pb], pb, nthreads=16)
+            assert np.array_equal(host(ct[:2048 * pb]), want_b)
+            c.decrypt_ragged(buf, buf, d_off, d_nb, n)
+            assert torch.equal(view.contiguous().reshape(-1), pt_b)
+        c.decrypt_ragged(want, want, d_off, d_nb, n)
+        assert torch.equal(want, src)
+    assert c.check() == ca.CYAES_OK
+    ref.close()
+    c.close()
+    torch.cuda.empty_cache()
+
+
 def test_dropin_size_zero_and_pieces():
     """The drop-in's argument rules: size 0 is a no-op whatever the
     pointers (the reference's loop never runs, cyr_rijndael.cpp:600), and a call
