@@ -39,6 +39,9 @@ __device__ __forceinline__ uint64_t rlane64(uint64_t v, uint32_t l) {
     return (uint64_t)hi << 32 | lo;
 }
 
+#ifndef CYAES_RAG_FULL_STEPS
+#define CYAES_RAG_FULL_STEPS 1  // 0: A/B variant, a regular group's full steps through the selects and masks too
+#endif
 #ifndef CYAES_DEC_RAGGED_DIV
 // The progress-feedback divisor: the short-launch one (a relay stream's ragged
 // decrypt has ~92 steps per wave; r06 A/B at 8 / 4 / 2: 1.161 / 1.153 / 1.144
@@ -192,7 +195,13 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
             // group's end loads row 0 lane 0's block (always valid) and its result
             // is never used (a valid lane's predecessor is valid).  A load under
             // `valid ? load : 0` joined the branches with a vmcnt(0) wait per row.
-            if (regular) {  // (as below: an invalid lane loads row 0 lane 0's block)
+            // A full step of a regular group (every step but a group's last): every lane valid,
+            // loads and stores without selects or exec masks.
+            const bool rfull = CYAES_RAG_FULL_STEPS && regular && base + 64 * R <= total;
+            if (rfull) {
+#pragma unroll
+                for (int k = 0; k < R; k++) c[k] = LD16U(gin + o32[k], re[k]);
+            } else if (regular) {  // (as below: an invalid lane loads row 0 lane 0's block)
                 const uint32_t safe32 = __builtin_amdgcn_readlane(o32[0], 0);
 #pragma unroll
                 for (int k = 0; k < R; k++) c[k] = LD16U(gin + (valid[k] ? o32[k] : safe32), re[k]);
@@ -266,11 +275,20 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_ragged(DecArgs a) {
             // went out 4-8 at a time (320 / 158 s_waitcnt per 640 reads); with
             // it, and this TU's iterative-ILP scheduler, in bursts of 64 (13 / 31).
             __builtin_amdgcn_sched_barrier(0);
+            if (rfull) {
 #pragma unroll
-            for (int k = 0; k < R; k++) {
-                Ext we = re[k];
-                if constexpr (CYAES_BOUNDS_CHECK) we = ext(a.out + (we.lo - a.in), we.hi - we.lo);
-                if (valid[k]) ST16U(regular ? gout + o32[k] : a.out + orow[k], we, pv[k]);
+                for (int k = 0; k < R; k++) {
+                    Ext we = re[k];
+                    if constexpr (CYAES_BOUNDS_CHECK) we = ext(a.out + (we.lo - a.in), we.hi - we.lo);
+                    ST16U(gout + o32[k], we, pv[k]);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < R; k++) {
+                    Ext we = re[k];
+                    if constexpr (CYAES_BOUNDS_CHECK) we = ext(a.out + (we.lo - a.in), we.hi - we.lo);
+                    if (valid[k]) ST16U(regular ? gout + o32[k] : a.out + orow[k], we, pv[k]);
+                }
             }
             carry = make_uint4(rl63(c[R - 1].x), rl63(c[R - 1].y), rl63(c[R - 1].z), rl63(c[R - 1].w));
         }
