@@ -1201,6 +1201,40 @@ def test_ragged_encrypt_by_lines(torch, layout):
     torch.cuda.empty_cache()
 
 
+def test_mixed_relay_stream_against_golden(torch):
+    """bench.py's relay_stream.mixed, full size: config B's bytes as a relay
+    tunnel stream of 0xFF00-B chunks and the socket reads' tails (29,580
+    packets, payload at packet offset 12; relay_local.cpp:188-206) encrypted
+    then decrypted in place through the ragged entry points; whole-buffer
+    digests against tests/golden/relay_mixed.json (the oracle's ragged batch,
+    tests/golden/gen_relay_mixed.py).  Also forced onto the static split and
+    the one-lane encrypt, which must give the same bytes."""
+    import json
+    import bench
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "relay_mixed.json")))
+    offsets, nbytes, alloc = bench.mixed_stream_layout(g["chunk_bytes"])
+    assert (int(offsets.size), alloc) == (g["packets"], g["stream_bytes"])
+    d_off, d_nb = dev(torch, offsets), dev(torch, nbytes)
+    buf = empty(torch, alloc)
+    for env in ({}, {"CYAES_DEC_DYN": "0", "CYAES_QUAD_MAX_CHAINS": "0"}):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            c = ca.GpuContext(0)
+        finally:
+            _restore(old)
+        c.set_keys(K0)
+        c.fill_synthetic(buf, 0, alloc // 16, 16, oracle.PLAINTEXT_SEED)
+        assert _digest_hex(c, buf, alloc) == g["plain_digest"]
+        c.encrypt_ragged(buf, buf, d_off, d_nb, int(offsets.size))
+        assert _digest_hex(c, buf, alloc) == g["cipher_digest"], env
+        c.decrypt_ragged(buf, buf, d_off, d_nb, int(offsets.size))
+        assert _digest_hex(c, buf, alloc) == g["plain_digest"], env
+        assert c.check() == ca.CYAES_OK
+        c.close()
+    torch.cuda.empty_cache()
+
+
 def test_dropin_size_zero_and_pieces():
     """The drop-in's argument rules: size 0 is a no-op whatever the
     pointers (the reference's loop never runs, cyr_rijndael.cpp:600), and a call
