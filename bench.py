@@ -621,6 +621,46 @@ def main():
         if dist_on:
             dist.barrier()
         mt = max_over_ranks(time.perf_counter() - t0)
+        # duplex: this stream encrypted while a second one (its ciphertext) is
+        # decrypted, cyaes_gpu_duplex_ragged, against the two calls back to back
+        mbuf2 = torch.empty_like(mbuf)
+        ctx.fill_synthetic(mbuf, 0, alloc // 16, 16, PLAINTEXT_SEED, sh)
+        ctx.fill_synthetic(mbuf2, 0, alloc // 16, 16, PLAINTEXT_SEED, sh)
+        ctx.encrypt_ragged(mbuf2, mbuf2, d_off, d_nb, n, stream=sh)
+
+        def m_dup():
+            ctx.duplex_ragged(mbuf, mbuf, d_off, d_nb, n, mbuf2, mbuf2, d_off, d_nb, n, stream=sh)
+        dpar = None
+        if not args.no_verify:
+            m_dup()
+            ok = ctx.check() == ca.CYAES_OK and dig() == gm["cipher_digest"]
+            ok = ok and ["%016x" % v for v in ctx.digest(mbuf2, alloc, sh)] == gm["plain_digest"]
+            dpar = "bit-exact" if all_ok(ok) else "MISMATCH"
+
+        def two():
+            m_enc()
+            m_dec()
+        dup_t = {}
+        for _ in range(args.packet_warmup):
+            m_dup()
+        for rnd in range(2):  # alternate order against the clock ramp
+            for name, fn in ((("two", two), ("duplex", m_dup)) if rnd == 0 else (("duplex", m_dup), ("two", two))):
+                if dist_on:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(args.packet_steps):
+                    fn()
+                torch.cuda.synchronize()
+                dup_t.setdefault(name, []).append(max_over_ranks(time.perf_counter() - t1) / args.packet_steps)
+        t_two, t_dup = min(dup_t["two"]), min(dup_t["duplex"])
+        duplex = {"ms": round(1e3 * t_dup, 4), "two_calls_ms": round(1e3 * t_two, 4),
+                  "value": round(2.0 * payload * world / t_dup / gib, 2), "unit": "GiB/s",
+                  "speedup": round(t_two / t_dup, 4), "parity": dpar,
+                  "note": "encrypt this stream while its ciphertext copy is decrypted (cyaes_gpu_duplex_ragged: packed "
+                          "encrypt, decrypt on the context's second stream) vs encrypt_ragged + decrypt_ragged; "
+                          "best of two rounds in alternating order, %d steps each" % args.packet_steps}
+        del mbuf2
         out = {
             "value": round(2.0 * payload * args.packet_steps * world / mt / gib, 2), "unit": "GiB/s",
             "encrypt_ms": round(sum(a.elapsed_time(b) for a, b, _ in mev) / args.packet_steps, 4),
@@ -631,6 +671,7 @@ def main():
                       "0xFF00-B chunks plus its tail, payload = chunk rounded to 16 at packet offset 12, packets back "
                       "to back, in place, cyaes_gpu_{en,de}crypt_ragged" % (CONFIGS["B"][0] * CONFIGS["B"][1]),
             "parity_note": "digest of the whole stream buffer vs tests/golden/relay_mixed.json (oracle)",
+            "duplex": duplex,
         }
         del mbuf, d_off, d_nb
         torch.cuda.empty_cache()

@@ -101,6 +101,8 @@ _SIGS = {
                                                 ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64,
                                                 ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                                 _vp]),
+    "cyaes_gpu_duplex_ragged": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, _vp,
+                                               _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp]),
     # include/cyaes_relay.h
     "cyaes_relay_round16": (ctypes.c_uint32, [ctypes.c_uint32]),
     "cyaes_relay_packet_bytes": (ctypes.c_uint32, [ctypes.c_uint32]),
@@ -382,6 +384,13 @@ class GpuContext:
         _check(self._lib.cyaes_gpu_duplex_uniform(self._h, _p(enc_in), _p(enc_out), enc_npayloads, enc_payload_bytes,
                                                   enc_key, _p(dec_in), _p(dec_out), dec_npayloads, dec_payload_bytes,
                                                   dec_key, _p(stream)), "duplex_uniform")
+
+    def duplex_ragged(self, enc_in, enc_out, enc_offsets, enc_nbytes, enc_npayloads, dec_in, dec_out, dec_offsets,
+                      dec_nbytes, dec_npayloads, enc_key=0, dec_key=0, stream=None):
+        """Encrypt one ragged relay stream and decrypt another (cyaes_gpu_duplex_ragged)."""
+        _check(self._lib.cyaes_gpu_duplex_ragged(self._h, _p(enc_in), _p(enc_out), _p(enc_offsets), _p(enc_nbytes),
+                                                 enc_npayloads, enc_key, _p(dec_in), _p(dec_out), _p(dec_offsets),
+                                                 _p(dec_nbytes), dec_npayloads, dec_key, _p(stream)), "duplex_ragged")
 
     def duplex_strided(self, enc_in, enc_out, enc_first, enc_stride, enc_npayloads, enc_payload_bytes, dec_in, dec_out,
                        dec_first, dec_stride, dec_npayloads, dec_payload_bytes, enc_key=0, dec_key=0, stream=None):

@@ -36,6 +36,8 @@ struct cyaes_gpu {
     bool strided_force = false; // env CYAES_STRIDED_FORCE=1: contiguous strided batches keep the strided kernels (A/B)
     bool dec_handoff = true;    // env CYAES_DEC_HANDOFF=0: in-place static decrypts snapshot their carries in a prepass
     bool duplex_off = false;    // env CYAES_DUPLEX=0: duplex calls run as two launches (tests, A/B)
+    int duplex_pack = 12;       // env CYAES_DUPLEX_PACK: waves per workgroup of cyaes_gpu_duplex_ragged's encrypt (A/B)
+    int dup_min_dec_wgs = 8;    // env CYAES_DUPLEX_DEC_WGS: least decrypt workgroups beside it (A/B)
     uint32_t duplex_dyn_pct = kDuplexDynPct;  // env CYAES_DUPLEX_DYN_PCT: the duplex decrypt's pool share (%)
     uint32_t* d_tables = nullptr;  // enc[512] | dec[512] | sbox[256 B]
     uint32_t* d_keys = nullptr;    // nkeys * kSchedWords
@@ -64,6 +66,10 @@ struct cyaes_gpu {
     hipEvent_t keys_written = nullptr;    // behind cyaes_gpu_set_keys_device's expansion on the caller's stream
     bool keys_written_pending = false;
     std::vector<uint32_t*> retired_keys;  // tables outgrown while batches may still read them; freed at destroy
+    // cyaes_gpu_duplex_ragged's second stream (created on first use: a
+    // context-lifetime stream takes a hardware queue)
+    std::mutex side_mu;
+    hipStream_t side = nullptr;
 };
 
 namespace {
@@ -171,6 +177,17 @@ Shape wave_shape(const cyaes_gpu* ctx, uint64_t waves, int max_threads) {
 
 }  // namespace
 
+// cyaes_gpu_duplex_ragged's packed encrypt: workgroups of about duplex_pack
+// waves, their count a multiple of the shader engines (32: workgroups go to
+// the XCDs in turn and to an XCD's four engines in turn, so the decrypt
+// beside it finds the same number of free CUs on every engine).
+constexpr int kDupUnit = 4 * (int)kXcds;
+static int packed_enc_wgs(const cyaes_gpu* ctx, uint64_t npayloads) {
+    const uint64_t qwaves = (4 * npayloads + 63) / 64, pw = (uint64_t)ctx->duplex_pack;
+    const uint64_t e = ((qwaves + pw - 1) / pw + kDupUnit - 1) / kDupUnit * kDupUnit;
+    return (int)std::min<uint64_t>(e, (uint64_t)std::max(kDupUnit, ctx->num_cus - kDupUnit));
+}
+
 bool cyaes::ragged_encrypt_is_quad(const cyaes_gpu* ctx, uint64_t n) {
     const uint64_t q = ctx->quad_max_chains;
     return n < (q > UINT64_MAX / kQuadRaggedFactor ? UINT64_MAX : q * kQuadRaggedFactor);
@@ -192,7 +209,7 @@ struct EncPlan {
 int enc_plan(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
              uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in,
              uint8_t* iv_out, const uint32_t* table, uint32_t table_keys, uint64_t off0, uint64_t stride,
-             EncPlan* plan) {
+             EncPlan* plan, bool pack = false) {
     EncArgs& a = plan->a;
     a = EncArgs{};
     plan->quad = plan->sess = false;
@@ -214,7 +231,16 @@ int enc_plan(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* of
     if (ragged ? ragged_encrypt_is_quad(ctx, npayloads) : npayloads < ctx->quad_max_chains) {
         // Latency-bound batch (fewer chains than lanes to fill the chip four
         // times over), or a ragged one: four lanes per chain (k_encrypt_quad).
-        const Shape sh = wave_shape(ctx, (4 * npayloads + 63) / 64, kEncThreads);
+        // pack (cyaes_gpu_duplex_ragged): ~12 waves per workgroup, on as few CUs
+        // as hold them, leaving the rest of the chip to a concurrent launch.
+        const uint64_t qwaves = (4 * npayloads + 63) / 64;
+        Shape sh;
+        if (pack) {
+            const uint64_t e = (uint64_t)packed_enc_wgs(ctx, npayloads);
+            sh = Shape{(int)e, (int)(64 * std::min<uint64_t>(16, (qwaves + e - 1) / e))};
+        } else {
+            sh = wave_shape(ctx, qwaves, kEncThreads);
+        }
         plan->quad = true;
         plan->grid = std::min(sh.grid, enc_grid_cap(ctx));
         plan->threads = sh.threads;
@@ -271,10 +297,10 @@ int encrypt_rag_lines(cyaes_gpu* ctx, const EncArgs& a, uint64_t nrag, hipStream
 int encrypt_common(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
                    uint64_t npayloads, uint32_t payload_bytes, const uint32_t* key_idx, uint32_t ppk,
                    const uint8_t* iv_in, uint8_t* iv_out, hipStream_t stream, const uint32_t* table = nullptr,
-                   uint32_t table_keys = 0, uint64_t off0 = 0, uint64_t stride = 0) {
+                   uint32_t table_keys = 0, uint64_t off0 = 0, uint64_t stride = 0, bool pack = false) {
     EncPlan plan;
     int st = enc_plan(ctx, in, out, offsets, nbytes, npayloads, payload_bytes, key_idx, ppk, iv_in, iv_out, table,
-                      table_keys, off0, stride, &plan);
+                      table_keys, off0, stride, &plan, pack);
     if (st) return st;
     // A strided batch for the lane kernel, unkeyed and without IV arrays: its
     // whole 1,024-payload groups are read by 64-B lines (k_encrypt_lines), the
@@ -604,7 +630,7 @@ int decrypt_uniform(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t np
 
 int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes,
                    uint64_t npayloads, const uint32_t* key_idx, uint32_t ppk, const uint8_t* iv_in, uint8_t* iv_out,
-                   hipStream_t stream, const uint32_t* table = nullptr, uint32_t table_keys = 0) {
+                   hipStream_t stream, const uint32_t* table = nullptr, uint32_t table_keys = 0, int max_grid = 0) {
     DecArgs a = {};
     int st = make_keysel(ctx, npayloads, key_idx, ppk, &a.keys, table, table_keys);
     if (st) return st;
@@ -641,7 +667,7 @@ int decrypt_ragged(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, const uint64
     a.nranges = (npayloads + a.group - 1) / a.group;
     if (a.nranges > 0xFFFFFFFFull) return CYAES_EINVAL;  // 32-bit tickets
     const Shape sh = wave_shape(ctx, a.nranges, kDecThreads);
-    const int grid = std::min(sh.grid, dec_grid_cap(ctx));
+    const int grid = std::min(std::min(sh.grid, dec_grid_cap(ctx)), max_grid > 0 ? max_grid : INT32_MAX);
     // Groups [0, nstat) static (strided over the waves), the rest a dynamic pool
     // from per-XCD ticket pools with stealing (as the flat kernel's ranges).
     const uint64_t nwaves = (uint64_t)grid * (sh.threads / 64);
@@ -747,6 +773,8 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* v = getenv("CYAES_STRIDED_FORCE")) ctx->strided_force = atoi(v) != 0;
     if (const char* v = getenv("CYAES_DEC_HANDOFF")) ctx->dec_handoff = atoi(v) != 0;
     if (const char* v = getenv("CYAES_DUPLEX")) ctx->duplex_off = atoi(v) == 0;
+    if (const char* v = getenv("CYAES_DUPLEX_PACK")) ctx->duplex_pack = std::max(1, std::min(16, atoi(v)));
+    if (const char* v = getenv("CYAES_DUPLEX_DEC_WGS")) ctx->dup_min_dec_wgs = std::max(1, atoi(v));
     if (const char* v = getenv("CYAES_DUPLEX_DYN_PCT")) ctx->duplex_dyn_pct = (uint32_t)strtoul(v, nullptr, 10);
     const HostTables& t = host_tables();
     uint8_t host[kTablesBytes];
@@ -788,6 +816,7 @@ int cyaes_gpu_destroy(cyaes_gpu* ctx) {
     }
     for (auto& u : ctx->key_uses) (void)hipEventDestroy(u.second);
     if (ctx->keys_written) (void)hipEventDestroy(ctx->keys_written);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     delete ctx;
     return map_err(e);
 }
@@ -1245,6 +1274,75 @@ int cyaes_gpu_duplex_strided(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d
     x.d = dp.a;
     CY_TRY(launch_duplex_lines(x, grid, s));
     return note_key_use(ctx, te, s);
+}
+
+// Duplex of two ragged relay streams (r06): the encrypt of a stream of few,
+// long payloads (0xFF00-B chunks: the quad kernel, bound by its chains'
+// latency) leaves most of the chip's LDS idle.  It runs packed
+// (16 waves per workgroup, on as few CUs as hold them) on `stream` while the
+// decrypt runs on the context's second stream, joined back into `stream`:
+// the decrypt takes the CUs the encrypt leaves.  Results as
+// cyaes_gpu_encrypt_ragged(enc, key row enc_key) then
+// cyaes_gpu_decrypt_ragged(dec, key row dec_key); other shapes run as those two
+// calls in that order.
+int cyaes_gpu_duplex_ragged(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d_enc_out, const uint64_t* d_enc_offsets,
+                            const uint32_t* d_enc_nbytes, uint64_t enc_npayloads, uint32_t enc_key,
+                            const uint8_t* d_dec_in, uint8_t* d_dec_out, const uint64_t* d_dec_offsets,
+                            const uint32_t* d_dec_nbytes, uint64_t dec_npayloads, uint32_t dec_key, void* stream) {
+    if (!ctx) return CYAES_EINVAL;
+    const bool has_e = enc_npayloads != 0, has_d = dec_npayloads != 0;
+    if (has_e && (!d_enc_offsets || !d_enc_nbytes || !ragged_args_ok(ctx, d_enc_in, d_enc_out, nullptr, nullptr)))
+        return CYAES_EINVAL;
+    if (has_d && (!d_dec_offsets || !d_dec_nbytes || !ragged_args_ok(ctx, d_dec_in, d_dec_out, nullptr, nullptr)))
+        return CYAES_EINVAL;
+    if ((has_e && enc_key >= ctx->nkeys) || (has_d && dec_key >= ctx->nkeys)) return CYAES_ERANGE;
+    if (!has_e && !has_d) return CYAES_OK;
+    DeviceGuard g(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t* te = ctx->d_keys + (uint64_t)enc_key * kSchedWords;
+    const uint32_t* td = ctx->d_keys + (uint64_t)dec_key * kSchedWords;
+    const bool concurrent = has_e && has_d && !ctx->duplex_off && ragged_encrypt_is_quad(ctx, enc_npayloads);
+    if (!concurrent) {
+        if (has_e) {
+            const int st = encrypt_common(ctx, d_enc_in, d_enc_out, d_enc_offsets, d_enc_nbytes, enc_npayloads, 0,
+                                          nullptr, 0, nullptr, nullptr, s, te, 1);
+            if (st) return st;
+        }
+        return has_d ? decrypt_ragged(ctx, d_dec_in, d_dec_out, d_dec_offsets, d_dec_nbytes, dec_npayloads, nullptr, 0,
+                                      nullptr, nullptr, s, td, 1)
+                     : CYAES_OK;
+    }
+    hipStream_t side;
+    {
+        std::lock_guard<std::mutex> lk(ctx->side_mu);
+        if (!ctx->side) CY_TRY(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        side = ctx->side;
+    }
+    hipEvent_t fork = nullptr, join = nullptr;
+    hipError_t e = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&join, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(fork, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);  // the decrypt starts after the caller's earlier work
+    int st = map_err(e);
+    if (st == CYAES_OK)
+        st = encrypt_common(ctx, d_enc_in, d_enc_out, d_enc_offsets, d_enc_nbytes, enc_npayloads, 0, nullptr, 0,
+                            nullptr, nullptr, s, te, 1, 0, 0, /*pack*/ true);
+    // The decrypt's workgroups (persistent) take only the CUs the encrypt's
+    // leave: whichever queue the dispatcher serves first, every workgroup of
+    // both launches is resident at once (a decrypt holding all CUs would
+    // otherwise start the encrypt's chains only as its pool drains).
+    const int dec_free = std::max(1, ctx->num_cus) - packed_enc_wgs(ctx, enc_npayloads);
+    const int dec_grid = std::max(ctx->dup_min_dec_wgs, dec_free / kDupUnit * kDupUnit);
+    if (st == CYAES_OK)
+        st = decrypt_ragged(ctx, d_dec_in, d_dec_out, d_dec_offsets, d_dec_nbytes, dec_npayloads, nullptr, 0, nullptr,
+                            nullptr, side, td, 1, dec_grid);
+    // join: the caller's stream waits for the decrypt (also on failure, for what was queued)
+    e = hipEventRecord(join, side);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+    if (st == CYAES_OK) st = map_err(e);
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+    return st;
 }
 
 int cyaes_gpu_check(cyaes_gpu* ctx) {

@@ -193,6 +193,24 @@ int cyaes_gpu_duplex_strided(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d
                              uint64_t dec_stride, uint64_t dec_npayloads, uint32_t dec_payload_bytes, uint32_t dec_key,
                              void* stream);
 
+/* Duplex of two ragged relay streams (device offset / size lists, as
+ * cyaes_gpu_{en,de}crypt_ragged): the stream a relay end sends and the one it
+ * receives.  Same results as
+ *   cyaes_gpu_encrypt_ragged(enc stream, key row enc_key)
+ *   cyaes_gpu_decrypt_ragged(dec stream, key row dec_key)
+ * in that order (no key arrays, no IV arrays), provided no byte of one
+ * stream's payloads is a byte of the other's.  A sent stream of few, long
+ * payloads (fewer than 131,072: 0xFF00-B chunks, whose CBC chains bound the
+ * encrypt by their latency) is encrypted on few CUs while the received one is
+ * decrypted on the others, concurrently (the decrypt on a second stream of the
+ * context, joined back into `stream`); other shapes run as the two calls.
+ * Errors as the ragged entry points; CYAES_ERANGE for a key row >= the number
+ * of keys set. */
+int cyaes_gpu_duplex_ragged(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d_enc_out, const uint64_t* d_enc_offsets,
+                            const uint32_t* d_enc_nbytes, uint64_t enc_npayloads, uint32_t enc_key,
+                            const uint8_t* d_dec_in, uint8_t* d_dec_out, const uint64_t* d_dec_offsets,
+                            const uint32_t* d_dec_nbytes, uint64_t dec_npayloads, uint32_t dec_key, void* stream);
+
 /* ---- Host-resident uniform batches (PCIe-inclusive) ----------------------
  * The relay path starts and ends in host memory (socket buffers).  These
  * process npayloads uniform payloads that live in HOST memory: chunks of

@@ -1235,6 +1235,77 @@ def test_mixed_relay_stream_against_golden(torch):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("shape", ["mixed", "mixed_pack4", "many_short", "empty_enc", "empty_dec", "off",
+                                   "keys"])
+def test_duplex_ragged_matches_two_ragged_calls(torch, shape):
+    """cyaes_gpu_duplex_ragged (the relay's sent stream encrypted,
+    relay_local.cpp:206, while its received stream is decrypted,
+    relay_server.cpp:329) against cyaes_gpu_encrypt_ragged then
+    cyaes_gpu_decrypt_ragged of reference contexts (one per key row),
+    bit-exact, bytes between payloads untouched: the mixed relay stream (few
+    long payloads: packed encrypt beside the decrypt on the context's second
+    stream, also at 4 waves per workgroup), many short payloads (the two
+    calls), an empty half, CYAES_DUPLEX=0, key rows 1 and 2; the sent stream
+    decrypts back; errors for a bad key row."""
+    import bench
+    keys = [K0, oracle.session_key(5), oracle.session_key(6)]
+    env = {"off": {"CYAES_DUPLEX": "0"}, "mixed_pack4": {"CYAES_DUPLEX_PACK": "4"}}.get(shape, {})
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        c = ca.GpuContext(0)
+    finally:
+        _restore(old)
+    c.set_keys(b"".join(keys))
+    ref = [ca.GpuContext(0) for _ in keys]
+    for r, k in zip(ref, keys):
+        r.set_keys(k)
+
+    def layout(kind, seed):
+        if kind == "mixed":
+            return bench.mixed_stream_layout(96 << 20, seed=seed)
+        if kind == "short":
+            rng = np.random.default_rng(seed)
+            nb = (16 * rng.integers(0, 93, 400000)).astype(np.uint32)
+            off = (np.cumsum(nb.astype(np.uint64) + 12) - nb).astype(np.uint64)
+            return off, nb, int(off[-1] + nb[-1]) + 16
+        return np.zeros(0, np.uint64), np.zeros(0, np.uint32), 16
+    ekind, dkind = {"many_short": ("short", "short"), "empty_enc": (None, "mixed"),
+                    "empty_dec": ("mixed", None)}.get(shape, ("mixed", "mixed"))
+    eo, en, ea = layout(ekind, 11)
+    do, dn, da = layout(dkind, 12)
+    ek, dk = (1, 2) if shape == "keys" else (0, 0)
+    e_buf, d_buf = empty(torch, (ea + 15) // 16 * 16), empty(torch, (da + 15) // 16 * 16)
+    c.fill_synthetic(e_buf, 3, e_buf.numel() // 16, 16, oracle.PLAINTEXT_SEED)
+    c.fill_synthetic(d_buf, 9, d_buf.numel() // 16, 16, oracle.PLAINTEXT_SEED)
+    de_o, de_n = (dev(torch, eo), dev(torch, en)) if en.size else (None, None)
+    dd_o, dd_n = (dev(torch, do), dev(torch, dn)) if dn.size else (None, None)
+    e_src = e_buf.clone()
+    want_e, want_d = e_buf.clone(), d_buf.clone()
+    if en.size:
+        ref[ek].encrypt_ragged(want_e, want_e, de_o, de_n, int(en.size))
+    if dn.size:
+        ref[dk].decrypt_ragged(want_d, want_d, dd_o, dd_n, int(dn.size))
+    for _ in range(2):  # the second call reuses the context's second stream
+        e_buf.copy_(e_src)
+        c.fill_synthetic(d_buf, 9, d_buf.numel() // 16, 16, oracle.PLAINTEXT_SEED)
+        c.duplex_ragged(e_buf, e_buf, de_o, de_n, int(en.size), d_buf, d_buf, dd_o, dd_n, int(dn.size),
+                        enc_key=ek, dec_key=dk)
+        assert torch.equal(e_buf, want_e), shape
+        assert torch.equal(d_buf, want_d), shape
+    if en.size:
+        ref[ek].decrypt_ragged(e_buf, e_buf, de_o, de_n, int(en.size))
+        assert torch.equal(e_buf, e_src)
+    with pytest.raises(ca.CyaesError):  # a bad key row of a non-empty half (an empty half's row is not read)
+        c.duplex_ragged(e_buf, e_buf, de_o, de_n, int(en.size), d_buf, d_buf, dd_o, dd_n, int(dn.size),
+                        enc_key=3 if en.size else 0, dec_key=0 if en.size else 3)
+    assert c.check() == ca.CYAES_OK
+    for r in ref:
+        r.close()
+    c.close()
+    torch.cuda.empty_cache()
+
+
 def test_dropin_size_zero_and_pieces():
     """The drop-in's argument rules: size 0 is a no-op whatever the
     pointers (the reference's loop never runs, cyr_rijndael.cpp:600), and a call

@@ -9,6 +9,9 @@ usage: python tools/ab_relay_env.py [--rounds 8] [--what duplex,mixed,ragged] SP
   mixed:  bench.py's mixed-size relay stream (mixed_stream_layout) through the
           ragged entry points, encrypt and decrypt in place.
   ragged: config B's relay stream through the ragged entry points.
+  mixdup: the mixed stream encrypted while a second copy is decrypted:
+          the two ragged calls, cyaes_gpu_duplex_ragged, and the duplex with a
+          one-packet decrypt (the packed encrypt alone).
 Prints per variant the median / min ms of each timed call and checks every
 variant's output against the first one's.
 """
@@ -67,12 +70,14 @@ def main():
         v1, v2 = b1[: n * stride].view(n, stride), b2[: n * stride].view(n, stride)
         d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride + hdr
         d_nb = torch.full((n,), pb, dtype=torch.int32, device="cuda")
-    if "mixed" in what:
+    if "mixed" in what or "mixdup" in what:
         offs, nbs, alloc = bench.mixed_stream_layout(n * pb)
         mn = int(offs.size)
         mbuf = torch.empty(alloc, dtype=torch.uint8, device="cuda")
         m_off = torch.from_numpy(offs.astype(np.int64)).to("cuda")
         m_nb = torch.from_numpy(nbs.astype(np.int32)).to("cuda")
+        if "mixdup" in what:
+            mbuf2 = torch.empty_like(mbuf)
     res = {spec: {} for spec, _ in ctxs}
     ref_out = {}
     for r in range(args.rounds + 1):
@@ -127,6 +132,30 @@ def main():
                     if k >= 2:
                         evs.setdefault("mix_enc", []).append(ea)
                         evs.setdefault("mix_dec", []).append(da)
+            if "mixdup" in what:
+                c.fill_synthetic(mbuf, 0, alloc // 16, 16, bench.PLAINTEXT_SEED)
+                c.fill_synthetic(mbuf2, 0, alloc // 16, 16, bench.PLAINTEXT_SEED)
+                c.encrypt_ragged(mbuf2, mbuf2, m_off, m_nb, mn)
+                if r == 0:  # parity once: the duplex gives the two calls' bytes
+                    c.duplex_ragged(mbuf, mbuf, m_off, m_nb, mn, mbuf2, mbuf2, m_off, m_nb, mn)
+                    d = (c.digest(mbuf, alloc), c.digest(mbuf2, alloc))
+                    c.decrypt_ragged(mbuf, mbuf, m_off, m_nb, mn)
+                    c.encrypt_ragged(mbuf2, mbuf2, m_off, m_nb, mn)
+                    ref_out.setdefault("mixdup", d)
+                    assert d == ref_out["mixdup"], spec
+                forms = [("two_calls", lambda: (c.encrypt_ragged(mbuf, mbuf, m_off, m_nb, mn),
+                                                c.decrypt_ragged(mbuf2, mbuf2, m_off, m_nb, mn))),
+                         ("duplex", lambda: c.duplex_ragged(mbuf, mbuf, m_off, m_nb, mn, mbuf2, mbuf2, m_off, m_nb,
+                                                            mn)),
+                         ("packed_enc", lambda: c.duplex_ragged(mbuf, mbuf, m_off, m_nb, mn, mbuf2, mbuf2, m_off,
+                                                                m_nb, 1))]
+                if r % 2:
+                    forms.reverse()
+                for name, fn in forms:
+                    for k in range(6):
+                        e = timed(fn)
+                        if k >= 3:
+                            evs.setdefault(name, []).append(e)
             torch.cuda.synchronize()
             if r == 0:
                 continue  # warm-up round
