@@ -13,6 +13,9 @@ namespace {
 
 template <bool RAGGED, bool KEYED, bool RUNS, bool SESS>
 __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt(EncArgs a) {
+    // The list k_encrypt_rag_lines handed back (a relay stream's is empty): no
+    // table image for nothing (5.9 us a launch, profiles/r06/final).
+    if (RAGGED && a.rest && *a.rest == 0) return;
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kEncLdsWords];
     fill_enc_image(lds_words, a.tables);
     __shared__ uint32_t lead;  // prio_feedback
@@ -44,7 +47,8 @@ __global__ __launch_bounds__(kEncThreads, 1) void k_encrypt_rag_lines(EncArgs a)
     if (threadIdx.x == 0) lead = 0;
     __syncthreads();
     CLOCK_PROBE(0);
-    rag_lines_walk(a, reinterpret_cast<const char*>(lds_words), &lead);
+    __shared__ uint32_t mpos[kEncThreads];  // per wave: its payloads' positions (rag_lines_walk)
+    rag_lines_walk(a, reinterpret_cast<const char*>(lds_words), &lead, mpos);
 }
 
 }  // namespace

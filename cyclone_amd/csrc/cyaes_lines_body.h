@@ -44,6 +44,15 @@ namespace {
 #ifndef CYAES_PROBE_LINES
 #define CYAES_PROBE_LINES 0  // cost probes only (wrong output): bit 1 stores at 16-B aligned positions
 #endif
+#ifndef CYAES_RAG_MPOS_LDS
+#define CYAES_RAG_MPOS_LDS 1  // 0: A/B variant, rag_lines_walk's member positions by four shuffles
+#endif
+#ifndef CYAES_RAG_BN_ZERO
+#define CYAES_RAG_BN_ZERO 1  // 0: A/B variant, the next-chunk registers undefined on an item's last chunk
+#endif
+#ifndef CYAES_RAG_META_PF
+#define CYAES_RAG_META_PF 1  // 0: A/B variant, rag_lines_walk loads an item's offsets and sizes at its start
+#endif
 #ifndef CYAES_LINES_PF
 #define CYAES_LINES_PF 1  // 0: A/B variant without the next item's prefetch
 #endif
@@ -199,7 +208,7 @@ __device__ __forceinline__ void lines_walk(const EncArgs& a, const char* lds, ui
 // leaves its payloads to the ragged lane kernel, which walks that list next
 // (enc_body, a.rest).  No prefetch of the next item's first chunk (the
 // members' positions of two items at once did not fit the registers).
-__device__ __forceinline__ void rag_lines_walk(const EncArgs& a, const char* lds, uint32_t* lead) {
+__device__ __forceinline__ void rag_lines_walk(const EncArgs& a, const char* lds, uint32_t* lead, uint32_t* mpos) {
     uint32_t prog = 0;
     const uint32_t lo = ((threadIdx.x & 31u) << 2) | 0x10000u;
     const uint32_t lane = threadIdx.x & 63u;
@@ -209,11 +218,29 @@ __device__ __forceinline__ void rag_lines_walk(const EncArgs& a, const char* lds
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb, gwaves = a.npayloads / 64u;
     const uintptr_t in0 = reinterpret_cast<uintptr_t>(a.in);
+    auto pl_of = [&](uint64_t g) { return (g >> 4) * 1024u + (g & 15u) + 16u * lane; };  // this lane's payload
+#if CYAES_RAG_META_PF
+    // the next item's offsets and sizes load during this item's chunks
+    uint64_t g = (uint64_t)blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t off_n = 0;
+    uint32_t nbr_n = 0;
+    if (g < gwaves) {
+        off_n = LD8(a.offsets + pl_of(g), ext(a.offsets, 8 * a.npayloads));
+        nbr_n = LD4(a.nbytes + pl_of(g), ext(a.nbytes, 4 * a.npayloads));
+    }
+    for (; g < gwaves; g += nwaves) {
+        const uint64_t off = off_n;
+        const uint32_t nb = nbr_n >> 4;
+        if (g + nwaves < gwaves) {
+            off_n = LD8(a.offsets + pl_of(g + nwaves), ext(a.offsets, 8 * a.npayloads));
+            nbr_n = LD4(a.nbytes + pl_of(g + nwaves), ext(a.nbytes, 4 * a.npayloads));
+        }
+#else
     for (uint64_t g = (uint64_t)blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); g < gwaves;
          g += nwaves) {
-        const uint64_t pl = (g >> 4) * 1024u + (g & 15u) + 16u * lane;  // this lane's payload
-        const uint64_t off = LD8(a.offsets + pl, ext(a.offsets, 8 * a.npayloads));
-        const uint32_t nb = LD4(a.nbytes + pl, ext(a.nbytes, 4 * a.npayloads)) >> 4;
+        const uint64_t off = LD8(a.offsets + pl_of(g), ext(a.offsets, 8 * a.npayloads));
+        const uint32_t nb = LD4(a.nbytes + pl_of(g), ext(a.nbytes, 4 * a.npayloads)) >> 4;
+#endif
         const uint32_t nb0 = __builtin_amdgcn_readfirstlane(nb);
         const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(in0 + off) & 63u);
         uint64_t wlo = off;
@@ -237,9 +264,22 @@ __device__ __forceinline__ void rag_lines_walk(const EncArgs& a, const char* lds
         // base: the lowest payload's first line (may precede a.in by < 64 B, inside its line)
         const uint8_t* base = a.in + (wlo - m);
         uint8_t* obase = a.out + (wlo - m);
-        uint32_t mrel[4];  // the group members' payloads (lanes k + 16 q): their first lines from base
+        // the group members' payloads (lanes k + 16 q): their first lines from
+        // base, through the wave's 256 B of LDS (one address and immediate
+        // offsets; lane-index registers for four shuffles were hoisted out of
+        // the walk and spilled)
+        uint32_t mrel[4];
+#if CYAES_RAG_MPOS_LDS
+        uint32_t* wpos = mpos + (threadIdx.x & ~63u);
+        wpos[lane] = (uint32_t)(off - wlo);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; q++) mrel[q] = wpos[(lane & 15u) + 16u * q];
+        __builtin_amdgcn_wave_barrier();
+#else
 #pragma unroll
         for (int q = 0; q < 4; q++) mrel[q] = (uint32_t)__shfl((int)(uint32_t)(off - wlo), (int)((lane & 15u) + 16u * q));
+#endif
         const uint32_t s = m >> 2;
         const uint32_t e = (s + 3u) & 3u, j0 = (s + 3u) >> 2;
         const uint32_t nlines = (m + 16u * nb0 + 63u) >> 6;
@@ -277,7 +317,14 @@ __device__ __forceinline__ void rag_lines_walk(const EncArgs& a, const char* lds
             else cut(std::integral_constant<int, 0>{});
             c0 = b[7].y, c1 = b[7].z, c2 = b[7].w;
             uint4 bn[8];
-            if (more) load_chunk(bn, t + 1);
+            if (more) {
+                load_chunk(bn, t + 1);
+            } else if (CYAES_RAG_BN_ZERO) {
+                // defined on the last chunk: left undefined, the registers were
+                // carried (and spilled, 22 VGPRs) from item to item
+#pragma unroll
+                for (int j = 0; j < 8; j++) bn[j] = make_uint4(0u, 0u, 0u, 0u);
+            }
             prio_feedback(lead, ++prog, kEncPrioDiv);
 #pragma unroll
             for (int j = 0; j < 8; j++) {
