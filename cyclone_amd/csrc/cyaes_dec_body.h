@@ -412,10 +412,19 @@ __device__ __forceinline__ void dec_flat_body(const DecArgs& a, const char* lds,
         asm volatile("" : "+s"(ka));
         if (ticket >= ka->nranges) break;
         const bool stat = ticket < ka->nstat;
-        const uint64_t begin = stat ? (uint64_t)ticket * ka->stat_blocks
-                                    : (uint64_t)ka->nstat * ka->stat_blocks +
-                                          (uint64_t)(ticket - ka->nstat) * ka->range_blocks;
-        const uint64_t end = min(begin + (stat ? ka->stat_blocks : ka->range_blocks), ka->nblocks);
+        uint64_t begin = stat ? (uint64_t)ticket * ka->stat_blocks
+                              : (uint64_t)ka->nstat * ka->stat_blocks + (uint64_t)(ticket - ka->nstat) * ka->range_blocks;
+        uint64_t end = min(begin + (stat ? ka->stat_blocks : ka->range_blocks), ka->nblocks);
+        if (ka->xw) {  // (A/B) the XCD-weighted split: this wave's one range in its slot's span
+            const uint32_t x = blockIdx.x % kXcds, wpx = nwaves / kXcds;
+            const uint64_t idx = (uint64_t)(blockIdx.x / kXcds) * (kDecThreads / 64) + (wave % (kDecThreads / 64));
+            uint64_t span0 = 0;
+            for (uint32_t y = 0; y < x; y++) span0 += (uint64_t)wpx * ka->xsteps[y];
+            const uint64_t len = (uint64_t)ka->xsteps[x] * (64 * R);
+            begin = min(span0 * (64 * R) + idx * len, ka->nblocks);
+            end = min(begin + len, ka->nblocks);
+            if (begin >= end) break;
+        }
         FlatPos ps;
         ps.bp = begin / a.bpp.d;
         ps.bpos = (uint32_t)(begin - ps.bp * a.bpp.d);

@@ -160,6 +160,11 @@ struct DecArgs {
     // with which the waves tag the boundary records they publish (dec_handoff,
     // cyaes_dec_body.h).
     uint64_t handoff;
+    // Flat kernel, XCD-weighted static split (A/B, env CYAES_DEC_XCD_W): one
+    // range per wave; the waves of workgroups b = x mod 8 take xsteps[x] steps
+    // each, the slots' spans laid out in slot order.
+    uint32_t xw;
+    uint32_t xsteps[kXcds];
 };
 
 // The duplex launch (cyaes_duplex_kernels.hip): one grid encrypts batch e,

@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
@@ -31,6 +32,7 @@ struct cyaes_gpu {
     uint32_t dec_range_steps = kDecRangeSteps;  // env CYAES_DEC_RANGE_STEPS: steps per dynamic flat-decrypt range
     uint32_t dec_groups_per_wave = kDecGroupsPerWave;  // env CYAES_DEC_GROUPS_PER_WAVE: ragged groups per wave
     uint32_t dec_dyn_pct = kDecDynPct;  // env CYAES_DEC_DYN_PCT: % of a decrypt's work in the dynamic pool
+    float dec_xcd_w[kXcds] = {};  // env CYAES_DEC_XCD_W=w0,...,w7: XCD-weighted static decrypt split (A/B; all 0: off)
     int dec_grid_max = 0;       // env CYAES_DEC_GRID: cap on decrypt workgroups (tests: many ranges per wave on small batches)
     bool strided_lists = false; // env CYAES_STRIDED_LISTS=1: strided decrypts as ragged batches (tests, A/B)
     bool strided_force = false; // env CYAES_STRIDED_FORCE=1: contiguous strided batches keep the strided kernels (A/B)
@@ -584,6 +586,19 @@ int dec_plan(cyaes_gpu* ctx, const uint8_t* in, uint8_t* out, uint64_t npayloads
         a.nstat = (uint32_t)std::min<uint64_t>(a.nranges, 0xFFFFFFFFull);
     }
     if (a.nranges > 0xFFFFFFFFull) return CYAES_EINVAL;  // 32-bit tickets (> 2^40 blocks)
+    // (A/B) XCD-weighted static split: out of place, static, one key, one range
+    // per wave, whole workgroups per slot
+    float wsum = 0.0f;
+    for (uint32_t x = 0; x < kXcds; x++) wsum += ctx->dec_xcd_w[x];
+    if (wsum > 0.0f && !a.dyn && in != out && !keyed_lane && !a.sess_blocks && !iv_in && !iv_out && grid_want <= 0 &&
+        grid % (int)kXcds == 0 && stride == 0) {
+        const uint64_t total = (nblocks + step - 1) / step, wpx = nwaves / kXcds;
+        for (uint32_t x = 0; x < kXcds; x++)
+            a.xsteps[x] = (uint32_t)std::ceil((double)total * ctx->dec_xcd_w[x] / wsum / (double)wpx);
+        a.xw = 1;
+        a.nstat = (uint32_t)nwaves;
+        a.nranges = nwaves;
+    }
     a.prio_short = fair_steps <= kDecShortSteps;
     a.bpp = make_fastdiv(bpp);
     a.step_q = (uint32_t)(step / bpp);
@@ -768,6 +783,11 @@ int cyaes_gpu_create(int device, cyaes_gpu** out) {
     if (const char* v = getenv("CYAES_DEC_RANGE_STEPS")) ctx->dec_range_steps = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_DEC_GROUPS_PER_WAVE")) ctx->dec_groups_per_wave = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_DEC_GRID")) ctx->dec_grid_max = atoi(v);
+    if (const char* v = getenv("CYAES_DEC_XCD_W")) {
+        float w[kXcds];
+        if (sscanf(v, "%f,%f,%f,%f,%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3], &w[4], &w[5], &w[6], &w[7]) == (int)kXcds)
+            for (uint32_t x = 0; x < kXcds; x++) ctx->dec_xcd_w[x] = std::max(0.0f, w[x]);
+    }
     if (const char* v = getenv("CYAES_DEC_DYN_PCT")) ctx->dec_dyn_pct = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("CYAES_STRIDED_LISTS")) ctx->strided_lists = atoi(v) != 0;
     if (const char* v = getenv("CYAES_STRIDED_FORCE")) ctx->strided_force = atoi(v) != 0;

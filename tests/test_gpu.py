@@ -1235,6 +1235,40 @@ def test_mixed_relay_stream_against_golden(torch):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("weights", ["1,1,1,1,1,1,1,1", "1.05,0.97,1.02,0.9,1.1,1,0.95,1.01", "1,0,3,1,1,0.5,2,0",
+                                     "0,0,0,0,0,0,0,1"])
+@pytest.mark.parametrize("n,pb", [(1 << 20, 1472), (262144, 65536 // 16), (300001, 1024), (4096, 1024), (7, 16)])
+def test_xcd_weighted_static_split(torch, weights, n, pb):
+    """The XCD-weighted static decrypt split (A/B, CYAES_DEC_XCD_W; VERDICT r05
+    next 7): every wave one range, workgroup slot x's waves w_x / sum(w) of
+    the steps, slots laid out in order, the last ranges clipped or empty; zero
+    weights leave a slot idle.  Out-of-place uniform decrypts against a context
+    with the equal split, bit-exact, and back to the plaintext
+    (cyr_rijndael.cpp:612-635)."""
+    old = {"CYAES_DEC_XCD_W": os.environ.get("CYAES_DEC_XCD_W")}
+    os.environ["CYAES_DEC_XCD_W"] = weights
+    try:
+        c = ca.GpuContext(0)
+    finally:
+        _restore(old)
+    ref = ca.GpuContext(0)
+    c.set_keys(K0)
+    ref.set_keys(K0)
+    pt = empty(torch, n * pb)
+    c.fill_synthetic(pt, 0, n, pb, oracle.PLAINTEXT_SEED)
+    ct = empty(torch, n * pb)
+    ref.encrypt_uniform(pt, ct, n, pb)
+    want, got = empty(torch, n * pb), empty(torch, n * pb)
+    ref.decrypt_uniform(ct, want, n, pb)
+    c.decrypt_uniform(ct, got, n, pb)
+    assert torch.equal(got, want), (weights, n, pb)
+    assert torch.equal(got, pt)
+    assert c.check() == ca.CYAES_OK
+    ref.close()
+    c.close()
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("shape", ["mixed", "mixed_pack4", "many_short", "empty_enc", "empty_dec", "off",
                                    "keys"])
 def test_duplex_ragged_matches_two_ragged_calls(torch, shape):
