@@ -62,6 +62,10 @@ using Clock = std::chrono::steady_clock;
 
 uint64_t up16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
+// A batch whose longest encrypt-type payload has at least this many bytes runs
+// its two directions side by side (cyaes::ragged_duplex_batch).
+constexpr uint32_t kDuplexMinChain = 16384;
+
 int map_err(hipError_t e) {
     if (e == hipSuccess) return CYAES_OK;
     return (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? CYAES_ENOMEM : CYAES_EDEVICE;
@@ -235,6 +239,7 @@ struct Stage {
     uint8_t* d_data = nullptr;
     hipEvent_t done = nullptr;  // recorded after the batch's scatter
     uint32_t ne = 0, nd = 0;
+    uint32_t emax = 0;   // the longest encrypt-type payload (bytes)
     uint64_t bytes = 0;  // payload bytes en/decrypted (stats)
     std::vector<Cb> cbs;
     std::vector<Seg> segs;
@@ -539,6 +544,7 @@ void cyaes_batcher::build_loop() {
         // Lay the batch out: shards in rotating order, each shard's requests in
         // submission order, until the stage's requests, data or bounce is full.
         st->ne = st->nd = 0;
+        st->emax = 0;
         st->bytes = 0;
         st->cbs.clear();
         st->segs.clear();
@@ -582,8 +588,12 @@ void cyaes_batcher::build_loop() {
                     }
                     bounce += bb;
                 }
-                if (d.op == cyaes::kOpEncrypt || d.op == cyaes::kOpRelaySeal) st->h_enc[st->ne++] = d;
-                else st->h_dec[st->nd++] = d;
+                if (d.op == cyaes::kOpEncrypt || d.op == cyaes::kOpRelaySeal) {
+                    st->h_enc[st->ne++] = d;
+                    st->emax = std::max(st->emax, d.crypt);
+                } else {
+                    st->h_dec[st->nd++] = d;
+                }
                 st->cbs.push_back(p.cb);
                 st->bytes += d.crypt;
             }
@@ -662,12 +672,20 @@ int cyaes_batcher::launch(Stage* st) {
         hand_off(prev);
     }
     int rc = map_err(e);
-    if (rc == CYAES_OK && ne)
-        rc = cyaes::ragged_batch(ctx, false, d_keys, key_cap, st->d_data, st->d_data, st->d_offs, st->d_nb, ne,
-                                 st->d_kid, pipe);
-    if (rc == CYAES_OK && nd)
-        rc = cyaes::ragged_batch(ctx, true, d_keys, key_cap, st->d_data, st->d_data, st->d_offs + ne, st->d_nb + ne,
-                                 nd, st->d_kid + ne, pipe);
+    // The batch's encrypt-type and decrypt-type lists: one after the other, or
+    // side by side when the encrypt has long chains (relay chunks of >= 16 KiB:
+    // its latency-bound chains leave most CUs to the decrypt).
+    if (rc == CYAES_OK && ne && nd && st->emax >= kDuplexMinChain)
+        rc = cyaes::ragged_duplex_batch(ctx, d_keys, key_cap, st->d_data, st->d_offs, st->d_nb, ne, st->d_kid,
+                                        st->d_offs + ne, st->d_nb + ne, nd, st->d_kid + ne, pipe);
+    else {
+        if (rc == CYAES_OK && ne)
+            rc = cyaes::ragged_batch(ctx, false, d_keys, key_cap, st->d_data, st->d_data, st->d_offs, st->d_nb, ne,
+                                     st->d_kid, pipe);
+        if (rc == CYAES_OK && nd)
+            rc = cyaes::ragged_batch(ctx, true, d_keys, key_cap, st->d_data, st->d_data, st->d_offs + ne,
+                                     st->d_nb + ne, nd, st->d_kid + ne, pipe);
+    }
     pending = st;  // (a failed batch still goes through flush / the next launch, with its status)
     return rc;
 }

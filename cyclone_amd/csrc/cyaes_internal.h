@@ -259,6 +259,13 @@ bool ragged_encrypt_is_quad(const cyaes_gpu* ctx, uint64_t n);
 int ragged_batch(cyaes_gpu* ctx, bool decrypt, const uint32_t* d_table, uint32_t table_keys, const uint8_t* in,
                  uint8_t* out, const uint64_t* offsets, const uint32_t* nbytes, uint64_t npayloads,
                  const uint32_t* key_idx, hipStream_t stream);
+// Both directions of a batcher batch over one stage (disjoint payloads): as
+// ragged_batch(encrypt) then ragged_batch(decrypt), the two run side by side
+// when the encrypt is a few long chains (cyaes_gpu_duplex_ragged's scheme).
+int ragged_duplex_batch(cyaes_gpu* ctx, const uint32_t* d_table, uint32_t table_keys, uint8_t* data,
+                        const uint64_t* e_off, const uint32_t* e_nb, uint64_t ne, const uint32_t* e_kidx,
+                        const uint64_t* d_off, const uint32_t* d_nb, uint64_t nd, const uint32_t* d_kidx,
+                        hipStream_t stream);
 
 // Host-memory registrations (cyaes_pins.cpp): every hipHostRegister the
 // library makes, in one process-wide registry.

@@ -1305,32 +1305,24 @@ int cyaes_gpu_duplex_strided(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d
 // cyaes_gpu_encrypt_ragged(enc, key row enc_key) then
 // cyaes_gpu_decrypt_ragged(dec, key row dec_key); other shapes run as those two
 // calls in that order.
-int cyaes_gpu_duplex_ragged(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d_enc_out, const uint64_t* d_enc_offsets,
-                            const uint32_t* d_enc_nbytes, uint64_t enc_npayloads, uint32_t enc_key,
-                            const uint8_t* d_dec_in, uint8_t* d_dec_out, const uint64_t* d_dec_offsets,
-                            const uint32_t* d_dec_nbytes, uint64_t dec_npayloads, uint32_t dec_key, void* stream) {
-    if (!ctx) return CYAES_EINVAL;
-    const bool has_e = enc_npayloads != 0, has_d = dec_npayloads != 0;
-    if (has_e && (!d_enc_offsets || !d_enc_nbytes || !ragged_args_ok(ctx, d_enc_in, d_enc_out, nullptr, nullptr)))
-        return CYAES_EINVAL;
-    if (has_d && (!d_dec_offsets || !d_dec_nbytes || !ragged_args_ok(ctx, d_dec_in, d_dec_out, nullptr, nullptr)))
-        return CYAES_EINVAL;
-    if ((has_e && enc_key >= ctx->nkeys) || (has_d && dec_key >= ctx->nkeys)) return CYAES_ERANGE;
-    if (!has_e && !has_d) return CYAES_OK;
-    DeviceGuard g(ctx->device);
-    hipStream_t s = (hipStream_t)stream;
-    const uint32_t* te = ctx->d_keys + (uint64_t)enc_key * kSchedWords;
-    const uint32_t* td = ctx->d_keys + (uint64_t)dec_key * kSchedWords;
-    const bool concurrent = has_e && has_d && !ctx->duplex_off && ragged_encrypt_is_quad(ctx, enc_npayloads);
+// The two ragged halves (validated), concurrently when the encrypt would run
+// on the quad kernel, else in order on `s`.  te / td: the key tables
+// (te_keys / td_keys rows) the halves' key index arrays select from (nullptr
+// arrays: row 0).
+static int duplex_ragged_impl(cyaes_gpu* ctx, const uint8_t* e_in, uint8_t* e_out, const uint64_t* e_off,
+                              const uint32_t* e_nb, uint64_t ne, const uint32_t* e_kidx, const uint8_t* d_in,
+                              uint8_t* d_out, const uint64_t* d_off, const uint32_t* d_nb, uint64_t nd,
+                              const uint32_t* d_kidx, const uint32_t* te, uint32_t te_keys, const uint32_t* td,
+                              uint32_t td_keys, hipStream_t s) {
+    const bool concurrent = ne && nd && !ctx->duplex_off && ragged_encrypt_is_quad(ctx, ne);
     if (!concurrent) {
-        if (has_e) {
-            const int st = encrypt_common(ctx, d_enc_in, d_enc_out, d_enc_offsets, d_enc_nbytes, enc_npayloads, 0,
-                                          nullptr, 0, nullptr, nullptr, s, te, 1);
+        if (ne) {
+            const int st = encrypt_common(ctx, e_in, e_out, e_off, e_nb, ne, 0, e_kidx, 0, nullptr, nullptr, s, te,
+                                          te_keys);
             if (st) return st;
         }
-        return has_d ? decrypt_ragged(ctx, d_dec_in, d_dec_out, d_dec_offsets, d_dec_nbytes, dec_npayloads, nullptr, 0,
-                                      nullptr, nullptr, s, td, 1)
-                     : CYAES_OK;
+        return nd ? decrypt_ragged(ctx, d_in, d_out, d_off, d_nb, nd, d_kidx, 0, nullptr, nullptr, s, td, td_keys)
+                  : CYAES_OK;
     }
     hipStream_t side;
     {
@@ -1345,24 +1337,45 @@ int cyaes_gpu_duplex_ragged(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d_
     if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);  // the decrypt starts after the caller's earlier work
     int st = map_err(e);
     if (st == CYAES_OK)
-        st = encrypt_common(ctx, d_enc_in, d_enc_out, d_enc_offsets, d_enc_nbytes, enc_npayloads, 0, nullptr, 0,
-                            nullptr, nullptr, s, te, 1, 0, 0, /*pack*/ true);
+        st = encrypt_common(ctx, e_in, e_out, e_off, e_nb, ne, 0, e_kidx, 0, nullptr, nullptr, s, te, te_keys, 0, 0,
+                            /*pack*/ true);
     // The decrypt's workgroups (persistent) take only the CUs the encrypt's
     // leave: whichever queue the dispatcher serves first, every workgroup of
     // both launches is resident at once (a decrypt holding all CUs would
     // otherwise start the encrypt's chains only as its pool drains).
-    const int dec_free = std::max(1, ctx->num_cus) - packed_enc_wgs(ctx, enc_npayloads);
+    const int dec_free = std::max(1, ctx->num_cus) - packed_enc_wgs(ctx, ne);
     const int dec_grid = std::max(ctx->dup_min_dec_wgs, dec_free / kDupUnit * kDupUnit);
     if (st == CYAES_OK)
-        st = decrypt_ragged(ctx, d_dec_in, d_dec_out, d_dec_offsets, d_dec_nbytes, dec_npayloads, nullptr, 0, nullptr,
-                            nullptr, side, td, 1, dec_grid);
+        st = decrypt_ragged(ctx, d_in, d_out, d_off, d_nb, nd, d_kidx, 0, nullptr, nullptr, side, td, td_keys,
+                            dec_grid);
     // join: the caller's stream waits for the decrypt (also on failure, for what was queued)
-    e = hipEventRecord(join, side);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
-    if (st == CYAES_OK) st = map_err(e);
+    if (join) {
+        e = hipEventRecord(join, side);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+        if (st == CYAES_OK) st = map_err(e);
+    }
     if (fork) (void)hipEventDestroy(fork);
     if (join) (void)hipEventDestroy(join);
     return st;
+}
+
+int cyaes_gpu_duplex_ragged(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d_enc_out, const uint64_t* d_enc_offsets,
+                            const uint32_t* d_enc_nbytes, uint64_t enc_npayloads, uint32_t enc_key,
+                            const uint8_t* d_dec_in, uint8_t* d_dec_out, const uint64_t* d_dec_offsets,
+                            const uint32_t* d_dec_nbytes, uint64_t dec_npayloads, uint32_t dec_key, void* stream) {
+    if (!ctx) return CYAES_EINVAL;
+    const bool has_e = enc_npayloads != 0, has_d = dec_npayloads != 0;
+    if (has_e && (!d_enc_offsets || !d_enc_nbytes || !ragged_args_ok(ctx, d_enc_in, d_enc_out, nullptr, nullptr)))
+        return CYAES_EINVAL;
+    if (has_d && (!d_dec_offsets || !d_dec_nbytes || !ragged_args_ok(ctx, d_dec_in, d_dec_out, nullptr, nullptr)))
+        return CYAES_EINVAL;
+    if ((has_e && enc_key >= ctx->nkeys) || (has_d && dec_key >= ctx->nkeys)) return CYAES_ERANGE;
+    if (!has_e && !has_d) return CYAES_OK;
+    DeviceGuard g(ctx->device);
+    return duplex_ragged_impl(ctx, d_enc_in, d_enc_out, d_enc_offsets, d_enc_nbytes, enc_npayloads, nullptr, d_dec_in,
+                              d_dec_out, d_dec_offsets, d_dec_nbytes, dec_npayloads, nullptr,
+                              ctx->d_keys + (uint64_t)enc_key * kSchedWords, 1,
+                              ctx->d_keys + (uint64_t)dec_key * kSchedWords, 1, (hipStream_t)stream);
 }
 
 int cyaes_gpu_check(cyaes_gpu* ctx) {
@@ -1423,6 +1436,22 @@ int cyaes_gpu_digest(const uint8_t* d_buf, uint64_t nbytes, uint64_t out[2], voi
 }
 
 }  // extern "C"
+
+// The batcher's two directions of one batch (cyaes_batcher.cpp launch): the
+// SEAL / ENCRYPT list and the OPEN / DECRYPT list over one stage, disjoint
+// payloads, per-request key rows of one table.
+int cyaes::ragged_duplex_batch(cyaes_gpu* ctx, const uint32_t* d_table, uint32_t table_keys, uint8_t* data,
+                               const uint64_t* e_off, const uint32_t* e_nb, uint64_t ne, const uint32_t* e_kidx,
+                               const uint64_t* d_off, const uint32_t* d_nb, uint64_t nd, const uint32_t* d_kidx,
+                               hipStream_t stream) {
+    if (!ctx || !d_table || (ne && (!e_off || !e_nb)) || (nd && (!d_off || !d_nb)) ||
+        !ragged_args_ok(ctx, data, data, nullptr, nullptr))
+        return CYAES_EINVAL;
+    if (!ne && !nd) return CYAES_OK;
+    DeviceGuard g(ctx->device);
+    return duplex_ragged_impl(ctx, data, data, e_off, e_nb, ne, e_kidx, data, data, d_off, d_nb, nd, d_kidx, d_table,
+                              table_keys, d_table, table_keys, stream);
+}
 
 // ---- host-memory drop-in (Rijndael::encrypt / decrypt) --------------------
 // Every call is one CBC chain (cyr_rijndael.cpp:588-635), synchronous, and a
