@@ -376,7 +376,10 @@ __device__ __forceinline__ void dec_handoff(const DecArgs& a, uint64_t wave, uin
 // progress word (*leadp, in the launch's work words) is zero.  KOFF: the byte
 // offset of these DecArgs inside the kernel's argument segment (0 for
 // k_decrypt_flat; the duplex kernel's arguments start with its EncArgs).
-template <bool KEYED, bool BIG, bool SESS, bool IV, bool STRIDED, uint32_t DIV, uint32_t KOFF>
+// XW: the XCD-weighted static split (A/B, DecArgs.xw) -- its own instantiation:
+// compiled into the others, the range code broke their LDS schedule (s_waitcnt
+// 232 -> 493 per step body, relay-stream decrypt +7.8 %).
+template <bool KEYED, bool BIG, bool SESS, bool IV, bool STRIDED, uint32_t DIV, uint32_t KOFF, bool XW = false>
 __device__ __forceinline__ void dec_flat_body(const DecArgs& a, const char* lds, uint32_t* leadp) {
     constexpr int R = kDecRows;
     uint32_t prog = 0;
@@ -415,7 +418,7 @@ __device__ __forceinline__ void dec_flat_body(const DecArgs& a, const char* lds,
         uint64_t begin = stat ? (uint64_t)ticket * ka->stat_blocks
                               : (uint64_t)ka->nstat * ka->stat_blocks + (uint64_t)(ticket - ka->nstat) * ka->range_blocks;
         uint64_t end = min(begin + (stat ? ka->stat_blocks : ka->range_blocks), ka->nblocks);
-        if (ka->xw) {  // (A/B) the XCD-weighted split: this wave's one range in its slot's span
+        if constexpr (XW) {  // (A/B) the XCD-weighted split: this wave's one range in its slot's span
             const uint32_t x = blockIdx.x % kXcds, wpx = nwaves / kXcds;
             const uint64_t idx = (uint64_t)(blockIdx.x / kXcds) * (kDecThreads / 64) + (wave % (kDecThreads / 64));
             uint64_t span0 = 0;

@@ -10,7 +10,7 @@
 namespace cyaes {
 namespace {
 
-template <bool KEYED, bool BIG, bool SESS, bool IV, bool STRIDED, uint32_t DIV>
+template <bool KEYED, bool BIG, bool SESS, bool IV, bool STRIDED, uint32_t DIV, bool XW = false>
 __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_words[kDecLdsWords];
     fill_dec_image(lds_words, a.tables);
@@ -18,7 +18,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_decrypt_flat(DecArgs a) {
     if (threadIdx.x == 0) *leadp = 0;
     __syncthreads();
     CLOCK_PROBE(1);
-    dec_flat_body<KEYED, BIG, SESS, IV, STRIDED, DIV, 0>(a, reinterpret_cast<const char*>(lds_words), leadp);
+    dec_flat_body<KEYED, BIG, SESS, IV, STRIDED, DIV, 0, XW>(a, reinterpret_cast<const char*>(lds_words), leadp);
 }
 
 // Before a decrypt (one small launch, stream-ordered): zero the launch's work
@@ -45,7 +45,9 @@ static void launch_flat(const DecArgs& a, dim3 g, dim3 b, hipStream_t stream) {
     const bool sess = a.sess_blocks != 0;  // keyed by step-aligned sessions: the unkeyed step per session
     const bool iv = a.iv_in != nullptr || a.iv_out != nullptr;  // (the runtime sets sess only without IVs)
     // STRIDED: unkeyed, no IV arrays (the runtime checks)
-    if (a.stride && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false, true, DIV>), g, b, 0, stream, a);
+    if (a.xw && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false, false, DIV, true>), g, b, 0, stream, a);
+    else if (a.xw) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false, false, DIV, true>), g, b, 0, stream, a);
+    else if (a.stride && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, false, false, true, DIV>), g, b, 0, stream, a);
     else if (a.stride) hipLaunchKernelGGL((k_decrypt_flat<false, false, false, false, true, DIV>), g, b, 0, stream, a);
     else if (sess && big) hipLaunchKernelGGL((k_decrypt_flat<false, true, true, false, false, DIV>), g, b, 0, stream, a);
     else if (sess) hipLaunchKernelGGL((k_decrypt_flat<false, false, true, false, false, DIV>), g, b, 0, stream, a);
