@@ -1235,6 +1235,51 @@ def test_mixed_relay_stream_against_golden(torch):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_duplex_ragged_random_layouts(torch, seed):
+    """cyaes_gpu_duplex_ragged on random tunnel-stream layouts (relay_local.cpp
+    :188-206 chunks of 0..0xFF00 B rounded to 16, random 4-B-aligned gaps,
+    empty payloads, random key rows; relay_server.cpp:329 decrypts the other
+    direction): against encrypt_ragged then decrypt_ragged of reference
+    contexts, bit-exact, the gaps untouched.  Few payloads take the concurrent
+    scheme (packed encrypt beside the decrypt); many take the two calls."""
+    rng = np.random.default_rng(1000 + seed)
+    keys = [oracle.session_key(20 + i) for i in range(3)]
+    c = ca.GpuContext(0)
+    c.set_keys(b"".join(keys))
+    ref = [ca.GpuContext(0) for _ in keys]
+    for r, k in zip(ref, keys):
+        r.set_keys(k)
+
+    def layout(n, maxb):
+        nb = (16 * ((rng.integers(0, maxb + 1, n) + 15) // 16)).astype(np.uint32)
+        nb[rng.random(n) < 0.05] = 0
+        gaps = (4 * rng.integers(0, 8, n)).astype(np.uint64)
+        pkt = gaps + nb.astype(np.uint64)
+        off = (np.cumsum(pkt) - nb.astype(np.uint64)).astype(np.uint64)
+        return off, nb, int(off[-1] + nb[-1]) + 64
+    ne = int(rng.choice([1, 7, 300, 2000, 40000]))
+    nd = int(rng.choice([1, 64, 5000, 30000]))
+    eo, en, ea = layout(ne, int(rng.choice([256, 4096, 0xFF00])) if ne < 40000 else 1500)
+    do, dn, da = layout(nd, int(rng.choice([256, 4096, 0xFF00])))
+    ek, dk = int(rng.integers(0, 3)), int(rng.integers(0, 3))
+    e_buf, d_buf = empty(torch, (ea + 15) // 16 * 16), empty(torch, (da + 15) // 16 * 16)
+    c.fill_synthetic(e_buf, seed, e_buf.numel() // 16, 16, oracle.PLAINTEXT_SEED)
+    c.fill_synthetic(d_buf, seed + 99, d_buf.numel() // 16, 16, oracle.PLAINTEXT_SEED)
+    de_o, de_n, dd_o, dd_n = dev(torch, eo), dev(torch, en), dev(torch, do), dev(torch, dn)
+    want_e, want_d = e_buf.clone(), d_buf.clone()
+    ref[ek].encrypt_ragged(want_e, want_e, de_o, de_n, ne)
+    ref[dk].decrypt_ragged(want_d, want_d, dd_o, dd_n, nd)
+    c.duplex_ragged(e_buf, e_buf, de_o, de_n, ne, d_buf, d_buf, dd_o, dd_n, nd, enc_key=ek, dec_key=dk)
+    assert torch.equal(e_buf, want_e), (seed, ne, nd)
+    assert torch.equal(d_buf, want_d), (seed, ne, nd)
+    assert c.check() == ca.CYAES_OK
+    for r in ref:
+        r.close()
+    c.close()
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("weights", ["1,1,1,1,1,1,1,1", "1.05,0.97,1.02,0.9,1.1,1,0.95,1.01", "1,0,3,1,1,0.5,2,0",
                                      "0,0,0,0,0,0,0,1"])
 @pytest.mark.parametrize("n,pb", [(1 << 20, 1472), (262144, 65536 // 16), (300001, 1024), (4096, 1024), (7, 16)])
