@@ -240,6 +240,7 @@ struct Stage {
     hipEvent_t done = nullptr;  // recorded after the batch's scatter
     uint32_t ne = 0, nd = 0;
     uint32_t emax = 0;   // the longest encrypt-type payload (bytes)
+    uint64_t dbytes = 0; // decrypt-type payload bytes
     uint64_t bytes = 0;  // payload bytes en/decrypted (stats)
     std::vector<Cb> cbs;
     std::vector<Seg> segs;
@@ -545,6 +546,7 @@ void cyaes_batcher::build_loop() {
         // submission order, until the stage's requests, data or bounce is full.
         st->ne = st->nd = 0;
         st->emax = 0;
+        st->dbytes = 0;
         st->bytes = 0;
         st->cbs.clear();
         st->segs.clear();
@@ -593,6 +595,7 @@ void cyaes_batcher::build_loop() {
                     st->emax = std::max(st->emax, d.crypt);
                 } else {
                     st->h_dec[st->nd++] = d;
+                    st->dbytes += d.crypt;
                 }
                 st->cbs.push_back(p.cb);
                 st->bytes += d.crypt;
@@ -674,10 +677,15 @@ int cyaes_batcher::launch(Stage* st) {
     int rc = map_err(e);
     // The batch's encrypt-type and decrypt-type lists: one after the other, or
     // side by side when the encrypt has long chains (relay chunks of >= 16 KiB:
-    // its latency-bound chains leave most CUs to the decrypt).
+    // its latency-bound chains leave most CUs to the decrypt).  dec_small: the
+    // decrypt's full-chip time (~1.4 GB/ms) under a sixth of the longest
+    // chain's (~0.6 us a block), too short to pay for a denser encrypt
+    // (the runtime then keeps the two launches unless packing costs nothing).
+    const double enc_us = st->emax / 16.0 * 0.6, dec_us = st->dbytes / 1.4e6;
     if (rc == CYAES_OK && ne && nd && st->emax >= kDuplexMinChain)
         rc = cyaes::ragged_duplex_batch(ctx, d_keys, key_cap, st->d_data, st->d_offs, st->d_nb, ne, st->d_kid,
-                                        st->d_offs + ne, st->d_nb + ne, nd, st->d_kid + ne, pipe);
+                                        st->d_offs + ne, st->d_nb + ne, nd, st->d_kid + ne, pipe,
+                                        dec_us * 6.0 < enc_us);
     else {
         if (rc == CYAES_OK && ne)
             rc = cyaes::ragged_batch(ctx, false, d_keys, key_cap, st->d_data, st->d_data, st->d_offs, st->d_nb, ne,

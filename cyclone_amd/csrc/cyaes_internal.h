@@ -265,7 +265,7 @@ int ragged_batch(cyaes_gpu* ctx, bool decrypt, const uint32_t* d_table, uint32_t
 int ragged_duplex_batch(cyaes_gpu* ctx, const uint32_t* d_table, uint32_t table_keys, uint8_t* data,
                         const uint64_t* e_off, const uint32_t* e_nb, uint64_t ne, const uint32_t* e_kidx,
                         const uint64_t* d_off, const uint32_t* d_nb, uint64_t nd, const uint32_t* d_kidx,
-                        hipStream_t stream);
+                        hipStream_t stream, bool dec_small);
 
 // Host-memory registrations (cyaes_pins.cpp): every hipHostRegister the
 // library makes, in one process-wide registry.

@@ -1313,8 +1313,16 @@ static int duplex_ragged_impl(cyaes_gpu* ctx, const uint8_t* e_in, uint8_t* e_ou
                               const uint32_t* e_nb, uint64_t ne, const uint32_t* e_kidx, const uint8_t* d_in,
                               uint8_t* d_out, const uint64_t* d_off, const uint32_t* d_nb, uint64_t nd,
                               const uint32_t* d_kidx, const uint32_t* te, uint32_t te_keys, const uint32_t* td,
-                              uint32_t td_keys, hipStream_t s) {
-    const bool concurrent = ne && nd && !ctx->duplex_off && ragged_encrypt_is_quad(ctx, ne);
+                              uint32_t td_keys, hipStream_t s, bool dec_small = false) {
+    // dec_small (the caller knows the decrypt is short beside the encrypt's
+    // longest chain): side by side only when packing leaves the encrypt's
+    // waves per CU as they are (few chains), since a denser encrypt runs
+    // ~9 % longer.
+    const uint64_t qwaves = (4 * ne + 63) / 64, cus = (uint64_t)std::max(1, ctx->num_cus);
+    const uint64_t ewgs = (uint64_t)std::max(1, packed_enc_wgs(ctx, ne));
+    const bool denser = (qwaves + ewgs - 1) / ewgs > (qwaves + cus - 1) / cus;
+    const bool concurrent =
+        ne && nd && !ctx->duplex_off && ragged_encrypt_is_quad(ctx, ne) && !(dec_small && denser);
     if (!concurrent) {
         if (ne) {
             const int st = encrypt_common(ctx, e_in, e_out, e_off, e_nb, ne, 0, e_kidx, 0, nullptr, nullptr, s, te,
@@ -1443,14 +1451,14 @@ int cyaes_gpu_digest(const uint8_t* d_buf, uint64_t nbytes, uint64_t out[2], voi
 int cyaes::ragged_duplex_batch(cyaes_gpu* ctx, const uint32_t* d_table, uint32_t table_keys, uint8_t* data,
                                const uint64_t* e_off, const uint32_t* e_nb, uint64_t ne, const uint32_t* e_kidx,
                                const uint64_t* d_off, const uint32_t* d_nb, uint64_t nd, const uint32_t* d_kidx,
-                               hipStream_t stream) {
+                               hipStream_t stream, bool dec_small) {
     if (!ctx || !d_table || (ne && (!e_off || !e_nb)) || (nd && (!d_off || !d_nb)) ||
         !ragged_args_ok(ctx, data, data, nullptr, nullptr))
         return CYAES_EINVAL;
     if (!ne && !nd) return CYAES_OK;
     DeviceGuard g(ctx->device);
     return duplex_ragged_impl(ctx, data, data, e_off, e_nb, ne, e_kidx, data, data, d_off, d_nb, nd, d_kidx, d_table,
-                              table_keys, d_table, table_keys, stream);
+                              table_keys, d_table, table_keys, stream, dec_small);
 }
 
 // ---- host-memory drop-in (Rijndael::encrypt / decrypt) --------------------

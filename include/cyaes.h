@@ -204,6 +204,9 @@ int cyaes_gpu_duplex_strided(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d
  * encrypt by their latency) is encrypted on few CUs while the received one is
  * decrypted on the others, concurrently (the decrypt on a second stream of the
  * context, joined back into `stream`); other shapes run as the two calls.
+ * Meant for two streams of comparable bytes: the CU split follows the sent
+ * stream's chain count, so a received stream far smaller than the sent one
+ * leaves the encrypt on fewer CUs than it would take alone (~9 % longer).
  * Errors as the ragged entry points; CYAES_ERANGE for a key row >= the number
  * of keys set. */
 int cyaes_gpu_duplex_ragged(cyaes_gpu* ctx, const uint8_t* d_enc_in, uint8_t* d_enc_out, const uint64_t* d_enc_offsets,
